@@ -1,0 +1,107 @@
+"""ctypes binding of libadmmq.so (the C-ABI of include/admmq.h).
+
+The product path has no CPU fallback: if the HIP library is missing or a tensor
+is not on a ROCm device, calls raise. Device memory, the current HIP stream and
+the workspace allocation come from PyTorch-ROCm (plumbing only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libadmmq.so")
+
+SCHEMES = {
+    "tensor_mseminmax_symmetric": 0,
+    "tensor_minmax": 1,
+    "tensor_symmetric": 2,
+    "tensor_affine": 3,
+}
+
+
+class AdmmProblem(ctypes.Structure):
+    _fields_ = [("F", ctypes.c_void_p), ("G", ctypes.c_void_p), ("H0", ctypes.c_void_p),
+                ("H_out", ctypes.c_void_p), ("U", ctypes.c_void_p), ("HT_out", ctypes.c_void_p),
+                ("X_out", ctypes.c_void_p), ("I", ctypes.c_int32), ("R", ctypes.c_int32)]
+
+
+class QTensor(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("rows", ctypes.c_int64),
+                ("cols", ctypes.c_int64), ("tmin", ctypes.c_float), ("tmax", ctypes.c_float),
+                ("has_minmax", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libadmmq.so once (raises loudly when it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"admmq: {LIB_PATH} is missing - build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "or `make -C admm-quantization_amd/csrc`; there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, S, I32, I64, F32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    sig = {
+        "admmq_admm_workspace_size": (S, [P, I32, I32]),
+        "admmq_admm_prepare": (I32, [P, I32, I32, P, S, P]),
+        "admmq_admm_run": (I32, [P, I32, I32, F32, I32, I32, I32, P, S, P, P]),
+        "admmq_admm_iteration_batched": (I32, [P, I32, I32, F32, I32, I32, I32, P, S, P, P]),
+        "admmq_quantize_workspace_size": (S, [P, I32, I32]),
+        "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
+        "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
+        "admmq_profile_begin": (I32, [I32]),
+        "admmq_profile_end": (I32, [P, P]),
+        "admmq_version": (I32, []),
+        "admmq_last_error": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().admmq_last_error().decode(errors="replace")
+        raise RuntimeError(f"admmq: {what} failed (status {rc}): {msg}")
+
+
+def require_device(*tensors: torch.Tensor):
+    for t in tensors:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"admmq: expected a torch.Tensor, got {type(t).__name__}")
+        if t.device.type != "cuda":
+            raise RuntimeError("admmq: tensors must live on a ROCm GPU (device 'cuda'); the MI355X path has "
+                               "no CPU implementation")
+        if t.dtype != torch.float32:
+            raise TypeError(f"admmq: float32 tensors required, got {t.dtype}")
+
+
+def stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def problems_array(items: Sequence[AdmmProblem]):
+    arr = (AdmmProblem * len(items))(*items)
+    return arr
+
+
+def qtensor_array(items: Sequence[QTensor]):
+    return (QTensor * len(items))(*items)

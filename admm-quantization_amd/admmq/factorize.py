@@ -1,0 +1,215 @@
+"""ALS driver of the ADMM quantized CP factorization (``scripts/factorize.py``).
+
+``factorize_layers`` runs the reference's per-layer loop (3-way
+``scripts/factorize.py:207-266``, 2-way ``:269-310``) for MANY independent layers at
+once: in each ALS sweep, mode m of every active layer is solved in one batched
+``admm_iteration_batched`` launch sequence, followed by one batched re-quantization.
+Per layer it keeps the reference's semantics exactly: modes in order A -> B -> C
+with each mode using the factors already updated in this sweep, duals carried
+across sweeps, the two reconstruction errors per sweep and the stop tests
+(|dloss| < tol, exploding error over 5 (3-way) or 10 (2-way) sweeps).
+
+``main()`` mirrors the reference CLI (same flag names) and output files
+(``{bits}bit_{qscheme}/factors_{method}_seed{seed}/{layer}_{method}_{init}_rank_{R}_mode_{n}.pt``
+plus ``_losshist.pt`` / ``_lossquanthist.pt``). Pretrained weights cannot be
+downloaded here, so weights come from ``--weights`` (a state_dict loaded with
+``weights_only=True``) or from the seeded synthetic generator of
+:mod:`admmq.synthetic`. The reference's own script crashes before reaching this
+loop; the intended 4-D -> 3-D reshape of ``:140-147`` is applied.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import synthetic
+from .admm import admm_iteration_batched, init_factors, squared_relative_diff
+from .quantization import quantize_batched
+
+
+def gram_mttkrp(W: torch.Tensor, factors: Sequence[torch.Tensor], mode: int):
+    """G (Gram∘Gram) and F (MTTKRP) of ``scripts/factorize.py:215-237`` / ``:276-287``.
+
+    F is computed as unfold(W, mode) @ KhatriRao(others) (one GEMM, no (I,J,R)
+    intermediate); G with the reference's own product order ``X^T X * (Y^T Y)``.
+    """
+    if W.dim() == 3:
+        A, B, C = factors
+        if mode == 0:
+            G = B.T @ B * (C.T @ C)
+            F = W.reshape(W.shape[0], -1) @ (B[:, None, :] * C[None, :, :]).reshape(-1, B.shape[1])
+        elif mode == 1:
+            G = A.T @ A * (C.T @ C)
+            F = W.permute(1, 0, 2).reshape(W.shape[1], -1) @ (A[:, None, :] * C[None, :, :]).reshape(-1, A.shape[1])
+        else:
+            G = A.T @ A * (B.T @ B)
+            F = W.permute(2, 0, 1).reshape(W.shape[2], -1) @ (A[:, None, :] * B[None, :, :]).reshape(-1, A.shape[1])
+        return G.contiguous(), F.contiguous()
+    A, B = factors
+    if mode == 0:
+        return (B.T @ B).contiguous(), (W @ B).contiguous()
+    return (A.T @ A).contiguous(), (W.T @ A).contiguous()
+
+
+def reconstruct(factors: Sequence[torch.Tensor]) -> torch.Tensor:
+    if len(factors) == 3:
+        return torch.einsum('ir,jr,kr->ijk', *factors)
+    return factors[0] @ factors[1].T
+
+
+@dataclass
+class LayerRun:
+    name: str
+    W: torch.Tensor
+    rank: int
+    factors: List[torch.Tensor]
+    duals: List[torch.Tensor] = field(default_factory=list)
+    quantized: List[Optional[torch.Tensor]] = field(default_factory=list)
+    loss: List[float] = field(default_factory=list)
+    lossq: List[float] = field(default_factory=list)
+    active: bool = True
+
+    def __post_init__(self):
+        if not self.duals:
+            self.duals = [torch.zeros_like(f) for f in self.factors]
+        if not self.quantized:
+            self.quantized = [None] * len(self.factors)
+
+
+def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: int, qscheme: str,
+              num_attempts: int = 200, record_errors: bool = True, tol: float = 1e-5):
+    """One ALS sweep over all active layers (modes batched across layers)."""
+    act = [r for r in runs if r.active]
+    nmodes = max((len(r.factors) for r in act), default=0)
+    for mode in range(nmodes):
+        sel = [r for r in act if mode < len(r.factors)]
+        probs = []
+        for r in sel:
+            G, F = gram_mttkrp(r.W, r.factors, mode)
+            probs.append((r.factors[mode], r.duals[mode], F, G))
+        Hs = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
+                                    check_spd=False)
+        for r, H in zip(sel, Hs):
+            r.factors[mode] = H
+        qs = quantize_batched(Hs, bits, qscheme, num_attempts=num_attempts)
+        for r, q in zip(sel, qs):
+            r.quantized[mode] = q
+    if not record_errors:
+        return
+    for r in act:
+        r.loss.append(squared_relative_diff(r.W, reconstruct(r.factors)))
+        r.lossq.append(squared_relative_diff(r.W, reconstruct(r.quantized)))
+        back = 5 if r.W.dim() == 3 else 10
+        if len(r.loss) > 1 and abs(r.loss[-2] - r.loss[-1]) < tol:
+            r.active = False
+        elif len(r.loss) > 10 and r.loss[-1] - r.loss[-back] > 1e-3:
+            r.active = False
+
+
+def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_iter_als: int, max_iter_admm: int,
+                     bits: int = 4, qscheme: str = "tensor_mseminmax_symmetric", init: str = "random", seed: int = 42,
+                     names: Optional[Sequence[str]] = None, eps: float = 1e-8, tol: float = 1e-5,
+                     num_attempts: int = 200, initial_factors=None) -> List[LayerRun]:
+    """``--method admm`` of scripts/factorize.py for a batch of layers."""
+    runs = []
+    for i, (W, R) in enumerate(zip(weights, ranks)):
+        fs = initial_factors[i] if initial_factors is not None else init_factors(W, rank=R, init=init, device=W.device,
+                                                                                 seed=seed)
+        fs = [f.contiguous().clone() for f in fs]
+        run = LayerRun(names[i] if names else f"layer{i}", W, R, fs)
+        if init != "random":   # scripts/factorize.py:192-204: record the starting point
+            q = quantize_batched(fs, bits, qscheme, num_attempts=num_attempts)
+            run.loss.append(squared_relative_diff(W, reconstruct(fs)))
+            run.lossq.append(squared_relative_diff(W, reconstruct(q)))
+        runs.append(run)
+    for _ in range(max_iter_als):
+        if not any(r.active for r in runs):
+            break
+        als_sweep(runs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts, tol=tol)
+    return runs
+
+
+def _layer_weight(args, device):
+    if args.weights:
+        sd = torch.load(args.weights, map_location="cpu", weights_only=True)
+        w = sd[args.layer + ".weight"].float()
+    else:
+        idx, spec = synthetic.find_layer(args.model_name, args.layer)
+        w = torch.from_numpy(synthetic.layer_weight(spec, idx))
+    if w.dim() == 4:   # intended reshape of scripts/factorize.py:140-147
+        w = w.reshape(w.shape[0], w.shape[1]) if w.shape[2:] == (1, 1) else w.reshape(w.shape[0], w.shape[1], -1)
+    if w.dim() not in (2, 3):
+        raise ValueError('Incorrect number of dimentions in weight tensor')
+    return w.to(device)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description="ADMM quantized CP factorization of one layer (MI355X)")
+    ap.add_argument("--model-name", type=str, required=True, help="[resnet18, resnet50, llama7b]")
+    ap.add_argument("--with-wandb", action="store_true", help="accepted for compatibility; logging is JSONL")
+    ap.add_argument("--method", type=str, required=True, help="[admm, parafac, parafac-epc]")
+    ap.add_argument("--init", type=str, default="random", help="[random, svd, parafac, parafac-epc]")
+    ap.add_argument("--layer", type=str, required=True)
+    ap.add_argument("--rank", type=int, required=False)
+    ap.add_argument("--reduction-rate", type=float, required=False)
+    ap.add_argument("--bits", type=int, required=True)
+    ap.add_argument("--max_iter_als", type=int, default=5000)
+    ap.add_argument("--max_iter_admm", type=int, default=1000)
+    ap.add_argument("--max_iter_epc", type=int, default=5000)
+    ap.add_argument("--seed", type=int, required=True)
+    ap.add_argument("--qscheme", type=str, required=True)
+    ap.add_argument("--weights", type=str, default=None, help="state_dict file (weights_only load); default synthetic")
+    ap.add_argument("--outdir-root", type=str, default=".")
+    args = ap.parse_args(argv)
+    if args.rank is None and args.reduction_rate is None:
+        raise ValueError('One of [--rank, --reduction-rate] arguments must be specified.')
+    if args.method not in ['admm', 'parafac', 'parafac-epc']:
+        raise ValueError('Method must be on of [admm, parafac, parafac-epc].')
+    return args
+
+
+def main(argv=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("admmq.factorize needs a ROCm GPU")
+    device = torch.device("cuda:0")
+    args = parse_args(argv)
+    torch.manual_seed(args.seed)
+    weight = _layer_weight(args, device)
+    if args.rank is None:
+        args.rank = int(weight.numel() / sum(list(weight.shape)) / args.reduction_rate)
+    outdir = os.path.join(args.outdir_root, f'{args.bits}bit_{args.qscheme}/factors_{args.method}_seed{args.seed}')
+    os.makedirs(outdir, exist_ok=True)
+    fileprefix = f'{args.layer}_{args.method}_{args.init}_rank_{args.rank}'
+    start = time.time()
+    if args.method == 'admm':
+        run = factorize_layers([weight], [args.rank], args.max_iter_als, args.max_iter_admm, args.bits, args.qscheme,
+                               args.init, args.seed, names=[args.layer])[0]
+        factors, factors_q = run.factors, run.quantized
+        torch.save(run.loss, os.path.join(outdir, fileprefix + '_losshist.pt'))
+        torch.save(run.lossq, os.path.join(outdir, fileprefix + '_lossquanthist.pt'))
+    else:
+        from .parafac_epc import parafac, parafac_epc
+        if args.method == 'parafac':
+            _, factors = parafac(weight, rank=args.rank, init=args.init, random_state=args.seed, tol=1e-8,
+                                 n_iter_max=args.max_iter_als)
+        else:
+            _, factors = parafac_epc(weight, rank=args.rank, init=args.init, als_maxiter=args.max_iter_als,
+                                     epc_maxiter=args.max_iter_epc)
+        factors = [f.float().contiguous() for f in factors]
+        factors_q = quantize_batched(factors, args.bits, args.qscheme)
+    print('Factorization took {} minutes'.format((time.time() - start) / 60))
+    for mode, factor in enumerate(factors):
+        torch.save(factor.cpu(), os.path.join(outdir, fileprefix + f'_mode_{mode}.pt'))
+    error = squared_relative_diff(weight, reconstruct(factors))
+    qerror = squared_relative_diff(weight, reconstruct(factors_q))
+    print('Factorization error is {} for usual and {} for quantized'.format(error, qerror))
+    return factors, factors_q
+
+
+if __name__ == "__main__":
+    main()

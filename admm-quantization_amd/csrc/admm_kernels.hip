@@ -1,0 +1,168 @@
+// ADMM per-call setup and per-iteration finalize (source/admm.py:51-67).
+//
+//   k_rho        rho = trace(G)/R                       (admm.py:53; trace accumulated in fp64 like torch-CPU)
+//   k_pack       padded Fp/H/U copies, P = F + rho(H+U)  (admm.py:56, first iteration's right-hand side)
+//   k_fill_a64   A = G + rho I in fp64 for the SPD inverse (admm.py:54)
+//   k_finalize   H = Q(X) with the chosen scale, U += H - H_T, next P = F + rho(H+U),
+//                residual sums for the r/s stop test  (admm.py:59-65)
+//   k_unpack     padded H/U -> caller tensors
+#include "quant_device.h"
+
+namespace admmq {
+
+__global__ __launch_bounds__(256) void k_rho(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.x];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < p.R; i += blockDim.x) s += (double)p.G_user[(size_t)i * p.R + i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // sequential-order fp64 sum is not required: trace of <= 1500 fp32 values is exact in fp64
+    const double tr = red[0] + red[1] + red[2] + red[3];
+    p.rho[0] = (float)tr / (float)p.R;
+    p.flags[0] = 0; p.flags[1] = 0; p.flags[2] = 0; p.flags[3] = 0;
+    for (int sl = 0; sl < 2; ++sl) {
+      p.stat[4 * sl + 0] = 0u; p.stat[4 * sl + 1] = 0xFFFFFFFFu; p.stat[4 * sl + 2] = 0u; p.stat[4 * sl + 3] = 0u;
+      for (int k = 0; k < 4; ++k) p.res[4 * sl + k] = 0.0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const float rho = p.rho[0];
+  const long long total = (long long)p.Ip * p.ld;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / p.ld), c = (int)(e - (long long)r * p.ld);
+    float f = 0.f, h = 0.f, u = 0.f, pv = 0.f;
+    if (r < p.I && c < p.R) {
+      const size_t o = (size_t)r * p.R + c;
+      f = p.F_user[o]; h = p.H0_user[o]; u = p.U_user[o];
+      pv = f + rho * (h + u);
+    }
+    p.Fp[e] = f; p.H[e] = h; p.U[e] = u; p.P[e] = pv; p.X[e] = 0.f; p.HT[e] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill_a64(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const float rho = p.rho[0];
+  const long long total = (long long)p.ldm * p.ldm;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / p.ldm), c = (int)(e - (long long)r * p.ldm);
+    double v;
+    if (r < p.R && c < p.R) {
+      const float g = p.G_user[(size_t)r * p.R + c];
+      v = (r == c) ? (double)(g + rho * 1.0f) : (double)(g + rho * 0.0f);   // G + rho*eye, in fp32
+    } else {
+      v = (r == c) ? 1.0 : 0.0;
+    }
+    p.A64[e] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restrict__ probs, const Chunk* __restrict__ chunks,
+                                                       int ncand, int bits, int scheme, int slot, int iter) {
+  const Chunk ck = chunks[blockIdx.x];
+  const ProbDesc& p = probs[ck.job];
+  if (p.flags[0]) return;
+  const QParams qp = block_qparams(scheme, bits, p.stat + 4 * slot, p.sse + (size_t)slot * ncand, ncand, 0, 0.f, 0.f);
+  const float rho = p.rho[0];
+  const long long total = (long long)p.I * p.ld;
+  const long long e = (long long)ck.start + 4LL * threadIdx.x;
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  if (e < total) {
+    const int row = (int)(e / p.ld);
+    const int c0 = (int)(e - (long long)row * p.ld);
+    const float4 x4 = *reinterpret_cast<const float4*>(p.X + e);
+    const float4 t4 = *reinterpret_cast<const float4*>(p.HT + e);
+    const float4 h4 = *reinterpret_cast<const float4*>(p.H + e);
+    const float4 u4 = *reinterpret_cast<const float4*>(p.U + e);
+    const float4 f4 = *reinterpret_cast<const float4*>(p.Fp + e);
+    const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, ts[4] = {t4.x, t4.y, t4.z, t4.w};
+    const float hs[4] = {h4.x, h4.y, h4.z, h4.w}, us[4] = {u4.x, u4.y, u4.z, u4.w};
+    const float fs[4] = {f4.x, f4.y, f4.z, f4.w};
+    float ho[4], uo[4], po[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (c0 + k < p.R) {
+        const float hn = apply_quant(xs[k], qp);          // H = quantize(H_T - U)
+        const float dh = hn - ts[k];
+        const float un = us[k] + dh;                      // U += H - H_T
+        ho[k] = hn; uo[k] = un;
+        po[k] = fs[k] + rho * (hn + un);                  // next rhs F + rho(H+U)
+        const float dp = hn - hs[k];
+        s1 += (double)(dh * dh); s2 += (double)(hn * hn);
+        s3 += (double)(dp * dp); s4 += (double)(un * un);
+      } else {
+        ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
+      }
+    }
+    *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
+    *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
+    *reinterpret_cast<float4*>(p.P + e) = make_float4(po[0], po[1], po[2], po[3]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off);
+    s3 += __shfl_xor(s3, off); s4 += __shfl_xor(s4, off);
+  }
+  __shared__ double red[4][4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[w][0] = s1; red[w][1] = s2; red[w][2] = s3; red[w][3] = s4; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double v = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[k][threadIdx.x];
+    atomicAdd(&p.res[4 * slot + threadIdx.x], v);
+  }
+  if (ck.start == 0 && threadIdx.x == 0) {
+    p.flags[1] = iter + 1;
+    unsigned* st = p.stat + 4 * (slot ^ 1);
+    st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
+    double* rs = p.res + 4 * (slot ^ 1);
+    rs[0] = 0.0; rs[1] = 0.0; rs[2] = 0.0; rs[3] = 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const long long total = (long long)p.I * p.R;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / p.R), c = (int)(e - (long long)r * p.R);
+    const size_t o = (size_t)r * p.ld + c;
+    p.H_out[e] = p.H[o];
+    p.U_user[e] = p.U[o];
+    if (p.HT_dbg) p.HT_dbg[e] = p.HT[o];
+    if (p.X_dbg) p.X_dbg[e] = p.X[o];
+  }
+}
+
+void launch_rho(const ProbDesc* d, int nprob, hipStream_t s) {
+  hipLaunchKernelGGL(k_rho, dim3(nprob), dim3(256), 0, s, d);
+}
+void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s) {
+  const long long tot = (long long)maxIp * maxld;
+  const int nb = (int)std::min<long long>(1024, (tot + 255) / 256);
+  hipLaunchKernelGGL(k_pack, dim3(nb, nprob), dim3(256), 0, s, d);
+}
+void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s) {
+  const long long tot = (long long)maxldm * maxldm;
+  const int nb = (int)std::min<long long>(1024, (tot + 255) / 256);
+  hipLaunchKernelGGL(k_fill_a64, dim3(nb, nprob), dim3(256), 0, s, d);
+}
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
+                          int slot, int iter, hipStream_t s) {
+  if (nchunks > 0)
+    hipLaunchKernelGGL(k_finalize_admm, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
+}
+void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s) {
+  const long long tot = (long long)maxI * maxR;
+  const int nb = (int)std::min<long long>(1024, (tot + 255) / 256);
+  hipLaunchKernelGGL(k_unpack, dim3(nb, nprob), dim3(256), 0, s, d);
+}
+
+}  // namespace admmq

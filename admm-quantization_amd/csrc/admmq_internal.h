@@ -1,0 +1,91 @@
+// Internal device/host structures of libadmmq (not part of the C-ABI).
+//
+// Memory layout in HBM (per ADMM problem = one (layer, mode) factor):
+//   Fp, H, U, P, X, HT : float32 [Ip x ld] row-major, ld = roundup(R,16),
+//                        Ip = roundup(I,32); every pad element is kept at exactly 0
+//   M                  : float32 [ldm x ldm], ldm = roundup(R,64); (G+rho I)^-1,
+//                        symmetric, zero outside the R x R block
+//   A64, L64           : float64 [ldm x ldm] SPD factor / inverse-factor scratch
+//   D64                : float64 [ldm x 32] diagonal Cholesky blocks
+//   stat[2][4]         : per parity slot {absmax bits, min enc, max enc, 0}
+//   sse[2][ncand]      : per parity slot, canonical fixed-point SSE per candidate
+//   res[2][4]          : per parity slot, fp64 residual sums S1..S4 (source/admm.py:62-63)
+//   flags[4]           : {done, iterations, spd_error, 0}
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace admmq {
+
+enum QScheme { kMse = 0, kMinMax = 1, kSymmetric = 2, kAffine = 3 };
+
+struct ProbDesc {
+  // caller buffers (I x R contiguous)
+  const float* F_user;
+  const float* G_user;
+  const float* H0_user;
+  float* H_out;
+  float* U_user;
+  float* HT_dbg;   // optional: last H_T (I x R)
+  float* X_dbg;    // optional: last H_T - U (I x R)
+  // internal padded buffers
+  float* Fp; float* H; float* U; float* P; float* X; float* HT;
+  float* M;
+  double* A64; double* L64; double* D64;   // D64: diagonal L blocks [nbk][32][32]
+  unsigned* stat;
+  unsigned long long* sse;
+  double* res;
+  int* flags;
+  float* rho;
+  int I, R, ld, Ip, ldm, nbk;
+  int nq;          // quads of the valid (I x R) region: I * ceil(R/4)
+  int pad_;
+};
+
+// A standalone quantization job (quantize_tensor): x viewed as (rows, cols).
+struct QJob {
+  const float* src;   // rows x cols contiguous (user)
+  float* dst;         // rows x cols contiguous (user)
+  float* Xp;          // padded copy rows x ld (workspace)
+  unsigned* stat;     // [4]
+  unsigned long long* sse;  // [ncand]
+  int rows, cols, ld, nq;
+  float tmin_kw, tmax_kw;   // affine kwargs (NaN = unset)
+  int has_kw, pad_;
+};
+
+// Work-unit tables (built on the host, uploaded once per call)
+struct GemmTile { int prob, tm, tn, first; };
+struct Chunk { int job, start; };
+
+// float <-> order-preserving unsigned encodings for atomicMin/Max
+__device__ __forceinline__ unsigned enc_ord(float f) {
+  unsigned b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float dec_ord(unsigned e) {
+  return __uint_as_float((e & 0x80000000u) ? (e & 0x7FFFFFFFu) : ~e);
+}
+
+// Host-side launchers (each defined in its own translation unit).
+void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
+void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
+void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
+void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps,
+                 int ncand, hipStream_t s);
+void launch_sse_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
+                     hipStream_t s);
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits,
+                          int qscheme, int slot, int iter, hipStream_t s);
+void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
+
+void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s);
+void launch_sse_q(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, hipStream_t s);
+void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
+                   hipStream_t s);
+
+constexpr int kSseQuads = 512;      // quads per SSE work unit (2048 elements, 8 KiB LDS)
+constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
+
+}  // namespace admmq

@@ -1,0 +1,375 @@
+// C-ABI of libadmmq: workspace planning and stream-ordered launch sequences.
+// See include/admmq.h for the contract and the reference interfaces replaced.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/admmq.h"
+#include "admmq_internal.h"
+
+namespace admmq {
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
+static int check_hip(const char* where) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(where) + ": " + hipGetErrorString(e);
+    return ADMMQ_ERR_HIP;
+  }
+  return ADMMQ_OK;
+}
+
+static int h2d(void* dst, const void* src, size_t n, hipStream_t s) {
+  if (n == 0) return ADMMQ_OK;
+  // pageable source: HIP stages it before returning, so the host vector may die afterwards
+  const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    g_err = std::string("upload: ") + hipGetErrorString(e);
+    return ADMMQ_ERR_HIP;
+  }
+  return ADMMQ_OK;
+}
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+static inline int rup(int v, int a) { return (v + a - 1) / a * a; }
+
+// Optional per-launch HIP-event timing (bench.py measures the dominant kernel live on
+// the stream it runs on). Events are created in admmq_profile_begin, never in a launch path.
+struct Prof {
+  bool on = false;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> cls;
+  size_t next = 0;
+};
+static Prof g_prof;
+
+static inline void prof_mark(hipStream_t s) {
+  if (!g_prof.on || g_prof.next >= g_prof.ev.size()) return;
+  (void)hipEventRecord(g_prof.ev[g_prof.next++], s);
+}
+static inline void prof_class(int c) {
+  if (g_prof.on && g_prof.next < g_prof.ev.size()) g_prof.cls.push_back(c);
+}
+
+// Carves the workspace in a fixed order so that size and run agree exactly.
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+  template <class T>
+  T* take(size_t n) {
+    off = align_up(off, 256);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+struct AdmmPlan {
+  std::vector<ProbDesc> desc;
+  std::vector<GemmTile> tiles;
+  std::vector<Chunk> sse_chunks, fin_chunks;
+  ProbDesc* d_desc = nullptr;
+  GemmTile* d_tiles = nullptr;
+  Chunk* d_sse = nullptr;
+  Chunk* d_fin = nullptr;
+  int32_t* d_info_tmp = nullptr;
+  size_t bytes = 0;
+  int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
+};
+
+static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
+  if (nprob <= 0 || !probs) return fail(ADMMQ_ERR_ARG, "no problems");
+  if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
+  Carver cv(ws);
+  pl.desc.resize(nprob);
+  for (int i = 0; i < nprob; ++i) {
+    const admmq_problem& a = probs[i];
+    if (a.I <= 0 || a.R <= 0) return fail(ADMMQ_ERR_ARG, "I and R must be positive");
+    if ((long long)a.I * a.R > (1LL << 30)) return fail(ADMMQ_ERR_ARG, "factor too large");
+    ProbDesc& d = pl.desc[i];
+    std::memset(&d, 0, sizeof(d));
+    d.F_user = a.F; d.G_user = a.G; d.H0_user = a.H0; d.H_out = a.H_out; d.U_user = a.U;
+    d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
+    d.I = a.I; d.R = a.R;
+    d.ld = rup(a.R, 16);
+    d.Ip = rup(a.I, 32);
+    d.ldm = rup(a.R, 64);
+    d.nbk = d.ldm / 32;
+    d.nq = a.I * ((a.R + 3) / 4);
+    const size_t fe = (size_t)d.Ip * d.ld;
+    d.Fp = cv.take<float>(fe); d.H = cv.take<float>(fe); d.U = cv.take<float>(fe);
+    d.P = cv.take<float>(fe); d.X = cv.take<float>(fe); d.HT = cv.take<float>(fe);
+    d.M = cv.take<float>((size_t)d.ldm * d.ldm);
+    d.A64 = cv.take<double>((size_t)d.ldm * d.ldm);
+    d.L64 = cv.take<double>((size_t)d.ldm * d.ldm);
+    d.D64 = cv.take<double>((size_t)d.ldm * 32);
+    d.stat = cv.take<unsigned>(8);
+    d.sse = cv.take<unsigned long long>(2 * (size_t)ncand);
+    d.res = cv.take<double>(8);
+    d.flags = cv.take<int>(4);
+    d.rho = cv.take<float>(4);
+    pl.maxIp = std::max(pl.maxIp, d.Ip); pl.maxld = std::max(pl.maxld, d.ld);
+    pl.maxldm = std::max(pl.maxldm, d.ldm); pl.maxnbk = std::max(pl.maxnbk, d.nbk);
+    pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
+  }
+  // GEMM tiles, longest K first (LPT over the grid); `first` marks tile (0,0).
+  pl.tiles.clear();
+  std::vector<int> order(nprob);
+  for (int i = 0; i < nprob; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    for (int tm = 0; tm < d.Ip / 32; ++tm)
+      for (int tn = 0; tn < (d.ld + 63) / 64; ++tn) pl.tiles.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
+  }
+  pl.sse_chunks.clear();
+  pl.fin_chunks.clear();
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
+    const long long tot = (long long)d.I * d.ld;
+    for (long long e = 0; e < tot; e += kElemChunk) pl.fin_chunks.push_back({i, (int)e});
+  }
+  pl.d_desc = cv.take<ProbDesc>(nprob);
+  pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
+  pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
+  pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
+  pl.bytes = align_up(cv.off, 256);
+  return ADMMQ_OK;
+}
+
+static int upload_admm(AdmmPlan& pl, hipStream_t s) {
+  int rc;
+  if ((rc = h2d(pl.d_desc, pl.desc.data(), pl.desc.size() * sizeof(ProbDesc), s))) return rc;
+  if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
+  if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
+  return check_hip("upload");
+}
+
+__global__ void k_export_info(const ProbDesc* __restrict__ d, int n, int32_t* info) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    info[4 * i + 0] = d[i].flags[1];
+    info[4 * i + 1] = d[i].flags[0];
+    info[4 * i + 2] = d[i].flags[2];
+    info[4 * i + 3] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Standalone quantization
+struct QPlan {
+  std::vector<QJob> jobs;
+  std::vector<Chunk> pack_chunks, sse_chunks;
+  QJob* d_jobs = nullptr;
+  Chunk* d_pack = nullptr;
+  Chunk* d_sse = nullptr;
+  size_t bytes = 0;
+};
+
+static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan& pl) {
+  if (n <= 0 || !t) return fail(ADMMQ_ERR_ARG, "no tensors");
+  if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
+  Carver cv(ws);
+  pl.jobs.resize(n);
+  for (int i = 0; i < n; ++i) {
+    QJob& j = pl.jobs[i];
+    std::memset(&j, 0, sizeof(j));
+    if (t[i].rows <= 0 || t[i].cols <= 0) return fail(ADMMQ_ERR_ARG, "empty tensor");
+    j.src = t[i].x; j.dst = t[i].y;
+    j.rows = (int)t[i].rows; j.cols = (int)t[i].cols;
+    j.ld = rup(j.cols, 4);
+    if ((long long)j.rows * j.ld >= (1LL << 31)) return fail(ADMMQ_ERR_ARG, "tensor too large");
+    j.nq = j.rows * (j.ld / 4);
+    j.has_kw = t[i].has_minmax; j.tmin_kw = t[i].tmin; j.tmax_kw = t[i].tmax;
+    j.Xp = cv.take<float>((size_t)j.rows * j.ld);
+    j.stat = cv.take<unsigned>(4);
+    j.sse = cv.take<unsigned long long>(ncand);
+  }
+  pl.pack_chunks.clear();
+  pl.sse_chunks.clear();
+  for (int i = 0; i < n; ++i) {
+    const QJob& j = pl.jobs[i];
+    const long long tot = (long long)j.rows * j.ld;
+    for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
+    for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
+  }
+  pl.d_jobs = cv.take<QJob>(n);
+  pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
+  pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
+  pl.bytes = align_up(cv.off, 256);
+  return ADMMQ_OK;
+}
+
+__global__ void k_qinit(QJob* jobs, int n, int ncand) {
+  const QJob& j = jobs[blockIdx.x];
+  for (int c = threadIdx.x; c < ncand; c += blockDim.x) j.sse[c] = 0ull;
+  if (threadIdx.x == 0) { j.stat[0] = 0u; j.stat[1] = 0xFFFFFFFFu; j.stat[2] = 0u; j.stat[3] = 0u; }
+}
+
+__global__ void k_copy_sse(const QJob* jobs, int ncand, unsigned long long* out) {
+  for (int c = threadIdx.x; c < ncand; c += blockDim.x) out[c] = jobs[0].sse[c];
+}
+
+static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStream_t s, bool final_pass) {
+  int rc;
+  if ((rc = h2d(pl.d_jobs, pl.jobs.data(), n * sizeof(QJob), s))) return rc;
+  if ((rc = h2d(pl.d_pack, pl.pack_chunks.data(), pl.pack_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
+  hipLaunchKernelGGL(k_qinit, dim3(n), dim3(256), 0, s, pl.d_jobs, n, ncand);
+  launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
+  if (qscheme == kMse) launch_sse_q(pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, s);
+  if (final_pass) launch_qfinal(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), ncand, bits, qscheme, s);
+  return check_hip("quantize");
+}
+
+}  // namespace admmq
+
+using namespace admmq;
+
+static int valid_scheme(int q) { return q >= 0 && q <= 3; }
+static int valid_bits(int b) { return b >= 1 && b <= 16; }
+
+extern "C" {
+
+int32_t admmq_version(void) { return 100; }
+
+int32_t admmq_profile_begin(int32_t max_launches) {
+  if (g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling already active");
+  g_prof.ev.resize(2 * (size_t)std::max(max_launches, 1));
+  for (auto& e : g_prof.ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(ADMMQ_ERR_HIP, "hipEventCreate");
+  g_prof.cls.clear();
+  g_prof.next = 0;
+  g_prof.on = true;
+  return ADMMQ_OK;
+}
+
+int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class) {
+  if (!g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling not active");
+  g_prof.on = false;
+  for (int c = 0; c < 4; ++c) { ms_per_class[c] = 0.0; launches_per_class[c] = 0; }
+  const size_t pairs = std::min(g_prof.next / 2, g_prof.cls.size());
+  int rc = ADMMQ_OK;
+  if (pairs > 0 && hipEventSynchronize(g_prof.ev[2 * pairs - 1]) != hipSuccess) rc = fail(ADMMQ_ERR_HIP, "sync");
+  for (size_t i = 0; rc == ADMMQ_OK && i < pairs; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess) { rc = ADMMQ_ERR_HIP; break; }
+    ms_per_class[g_prof.cls[i]] += ms;
+    launches_per_class[g_prof.cls[i]] += 1;
+  }
+  for (auto& e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof.ev.clear();
+  g_prof.cls.clear();
+  return rc;
+}
+
+const char* admmq_last_error(void) { return g_err.c_str(); }
+
+size_t admmq_admm_workspace_size(const admmq_problem* probs, int32_t nprob, int32_t num_attempts) {
+  AdmmPlan pl;
+  if (plan_admm(probs, nprob, num_attempts, nullptr, pl) != ADMMQ_OK) return 0;
+  return pl.bytes;
+}
+
+int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  AdmmPlan pl;
+  int rc = plan_admm(probs, nprob, num_attempts, workspace, pl);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if ((rc = upload_admm(pl, s))) return rc;
+  prof_class(3); prof_mark(s);
+  launch_rho(pl.d_desc, nprob, s);
+  launch_pack(pl.d_desc, nprob, pl.maxIp, pl.maxld, s);
+  launch_fill_a64(pl.d_desc, nprob, pl.maxldm, s);
+  launch_spd_inverse(pl.d_desc, nprob, pl.maxnbk, s);
+  prof_mark(s);
+  return check_hip("admm_prepare");
+}
+
+int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
+                       int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
+                       int32_t* info, void* stream) {
+  if (!valid_scheme(qscheme)) return fail(ADMMQ_ERR_SCHEME, "unknown qscheme");
+  if (!valid_bits(bits)) return fail(ADMMQ_ERR_ARG, "bits out of range");
+  AdmmPlan pl;
+  int rc = plan_admm(probs, nprob, num_attempts, workspace, pl);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int ntiles = (int)pl.tiles.size(), nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
+  for (int it = 0; it + 1 < max_iter; ++it) {
+    const int slot = it & 1;
+    prof_class(0); prof_mark(s);
+    launch_gemm(pl.d_desc, pl.d_tiles, ntiles, slot, it, eps, num_attempts, s);
+    prof_mark(s);
+    if (qscheme == kMse) {
+      prof_class(1); prof_mark(s);
+      launch_sse_admm(pl.d_desc, pl.d_sse, nsse, num_attempts, bits, slot, s);
+      prof_mark(s);
+    }
+    prof_class(2); prof_mark(s);
+    launch_finalize_admm(pl.d_desc, pl.d_fin, nfin, num_attempts, bits, qscheme, slot, it, s);
+    prof_mark(s);
+  }
+  if (max_iter > 1) launch_unpack(pl.d_desc, nprob, pl.maxI, pl.maxR, s);
+  if (info) hipLaunchKernelGGL(k_export_info, dim3((nprob + 63) / 64), dim3(64), 0, s, pl.d_desc, nprob, info);
+  return check_hip("admm_run");
+}
+
+int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
+                                     int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,
+                                     size_t workspace_bytes, int32_t* info, void* stream) {
+  int rc = admmq_admm_prepare(probs, nprob, num_attempts, workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  return admmq_admm_run(probs, nprob, max_iter, eps, bits, qscheme, num_attempts, workspace, workspace_bytes, info,
+                        stream);
+}
+
+size_t admmq_quantize_workspace_size(const admmq_qtensor* t, int32_t n, int32_t num_attempts) {
+  QPlan pl;
+  if (plan_quant(t, n, num_attempts, nullptr, pl) != ADMMQ_OK) return 0;
+  return pl.bytes;
+}
+
+int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, int32_t qscheme, int32_t num_attempts,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  if (!valid_scheme(qscheme)) return fail(ADMMQ_ERR_SCHEME, "unknown qscheme");
+  if (!valid_bits(bits)) return fail(ADMMQ_ERR_ARG, "bits out of range");
+  QPlan pl;
+  int rc = plan_quant(t, n, num_attempts, workspace, pl);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  return run_quant(pl, n, bits, qscheme, num_attempts, static_cast<hipStream_t>(stream), true);
+}
+
+int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,
+                            uint64_t* sse_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!valid_bits(bits)) return fail(ADMMQ_ERR_ARG, "bits out of range");
+  admmq_qtensor t;
+  std::memset(&t, 0, sizeof(t));
+  t.x = x; t.y = nullptr; t.rows = rows; t.cols = cols;
+  QPlan pl;
+  int rc = plan_quant(&t, 1, num_attempts, workspace, pl);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if ((rc = run_quant(pl, 1, bits, kMse, num_attempts, s, false))) return rc;
+  hipLaunchKernelGGL(k_copy_sse, dim3(1), dim3(256), 0, s, pl.d_jobs, num_attempts,
+                     reinterpret_cast<unsigned long long*>(sse_out));
+  return check_hip("mse_sse_table");
+}
+
+}  // extern "C"

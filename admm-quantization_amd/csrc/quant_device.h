@@ -1,0 +1,251 @@
+// Device-side quantizer arithmetic shared by the ADMM projection (admm_kernels.hip)
+// and standalone quantize_tensor (quant_kernels.hip).
+//
+// Every operation below is a float32 IEEE operation in the same order as the
+// reference's torch-CPU code (source/quantization.py), compiled with
+// -ffp-contract=off so no multiply/add pair is fused behind our back.
+#pragma once
+#include "admmq_internal.h"
+
+namespace admmq {
+
+// torch.linspace(0.2*mx.item(), 1.2*mx.item(), n)[c]   (source/quantization.py:130)
+// Pinned by tests/golden/f5_linspace.npz: fma(step, c, start) below n/2,
+// fma(-step, n-1-c, end) above.
+__device__ __forceinline__ float cand_t(float mx, int c, int n) {
+  const float S = (float)(0.2 * (double)mx);
+  const float E = (float)(1.2 * (double)mx);
+  if (n == 1) return S;
+  const float step = (E - S) / (float)(n - 1);
+  if (c < (n >> 1)) return __builtin_fmaf(step, (float)c, S);
+  return __builtin_fmaf(-step, (float)(n - 1 - c), E);
+}
+
+__device__ __forceinline__ bool mse_degenerate(float mx) { return !(mx > 0.f && mx < __builtin_inff()); }
+
+// Fixed-point exponent of the canonical SSE rule (oracle/quant_oracle.py):
+// K = 56 - ceil_log2(nquads) - 2*E, mx = m*2^E with m in [0.5,1).
+__device__ __forceinline__ int fixed_exp(float mx, int nq) {
+  int e;
+  (void)__builtin_frexpf(mx, &e);
+  const int cl = (nq > 1) ? (32 - __builtin_clz((unsigned)(nq - 1))) : 0;
+  return 56 - cl - 2 * e;
+}
+
+// floor(g * 2^K) as uint64, exact (g >= 0 float32; the planner guarantees < 2^63).
+__device__ __forceinline__ unsigned long long to_fixed(float g, int K) {
+  const float v = __builtin_ldexpf(g, K);
+  const float vh = v * 0x1p-32f;
+  const unsigned hi = __float2uint_rz(vh);
+  const float r = v - (float)hi * 0x1p32f;           // exact: representable remainder
+  const unsigned lo = __float2uint_rz(r);
+  return ((unsigned long long)hi << 32) + (unsigned long long)lo;
+}
+
+struct QParams {
+  int scheme;
+  int bits;
+  float scale;
+  float qlo, qhi;
+  int zp;
+  float mn, rng, n;
+  int nan_all;
+};
+
+__device__ __forceinline__ float nan_clamp(float q, float lo, float hi) {
+  // torch.clamp propagates NaN; fmin/fmax would not.
+  return (q != q) ? q : __builtin_fminf(__builtin_fmaxf(q, lo), hi);
+}
+
+// int64 conversion of a float the way x86 torch-CPU does it (`.to(int)`): NaN /
+// out-of-range -> INT64_MIN.
+__device__ __forceinline__ long long to_i64_x86(float v) {
+  if (!(v == v) || v >= 9.2233720368547758e18f || v < -9.2233720368547758e18f) return (long long)0x8000000000000000ull;
+  return (long long)v;
+}
+__device__ __forceinline__ int to_i32_x86(float v) {
+  if (!(v == v) || v >= 2147483648.0f || v < -2147483648.0f) return (int)0x80000000u;
+  return (int)v;
+}
+
+// Parameters of the non-MSE schemes from tensor min/max (source/quantization.py:48-66, 91-106).
+__device__ __forceinline__ QParams qparams_stats(int scheme, int bits, float tmin, float tmax, int has_nan,
+                                                 int has_kw, float kw_min, float kw_max) {
+  QParams p;
+  p.scheme = scheme;
+  p.bits = bits;
+  p.nan_all = 0;
+  p.scale = 0.f; p.zp = 0; p.mn = 0.f; p.rng = 0.f; p.n = 0.f;
+  const int q = 1 << (bits - 1);
+  p.qlo = (float)(-q);
+  p.qhi = (float)(q - 1);
+  const float den = (float)(2 * q - 1);
+  if (has_nan) { tmin = __builtin_nanf(""); tmax = __builtin_nanf(""); }
+  if (scheme == kSymmetric) {
+    const float am = __builtin_fabsf(tmin);
+    const float m = (am > tmax) ? am : tmax;
+    p.scale = (2.0f * m) / den;
+  } else if (scheme == kAffine) {
+    if (has_kw) { tmin = kw_min; tmax = kw_max; }
+    p.scale = (tmax - tmin) / den;
+    const int t = to_i32_x86(tmin / p.scale);
+    int zp = (int)((unsigned)(-q) - (unsigned)t);   // int32 wrap like torch
+    zp = zp < -q ? -q : (zp > q - 1 ? q - 1 : zp);
+    p.zp = zp;
+  } else {  // kMinMax
+    p.mn = tmin;
+    p.rng = tmax - tmin;
+    p.n = (float)((1 << bits) - 1);
+  }
+  return p;
+}
+
+__device__ __forceinline__ QParams qparams_mse(int bits, float t) {
+  QParams p;
+  p.scheme = kMse;
+  p.bits = bits;
+  const int q = 1 << (bits - 1);
+  p.qlo = (float)(-q);
+  p.qhi = (float)(q - 1);
+  p.scale = (2.0f * t) / (float)(2 * q - 1);
+  p.nan_all = (t == t) ? 0 : 1;
+  p.zp = 0; p.mn = 0.f; p.rng = 0.f; p.n = 0.f;
+  return p;
+}
+
+__device__ __forceinline__ float apply_quant(float x, const QParams& p) {
+  if (p.scheme == kMse) {
+    if (p.nan_all) return __builtin_nanf("");
+    const float q = nan_clamp(__builtin_rintf(x / p.scale), p.qlo, p.qhi);
+    return q * p.scale;
+  }
+  if (p.scheme == kSymmetric) {
+    const float q = nan_clamp(__builtin_rintf(x / p.scale), p.qlo, p.qhi);
+    return (float)to_i64_x86(q) * p.scale;
+  }
+  if (p.scheme == kAffine) {
+    const float lv = nan_clamp(__builtin_rintf(x / p.scale) + (float)p.zp, p.qlo, p.qhi);
+    const long long li = to_i64_x86(lv);
+    const long long d = (long long)((unsigned long long)li - (unsigned long long)(long long)p.zp);
+    return (float)d * p.scale;
+  }
+  // kMinMax (source/quantization.py:48-66)
+  if (p.bits == 1) {
+    const float sg = (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : ((x == x) ? 0.f : x));
+    return sg - 1.f;
+  }
+  const float r = (x - p.mn) / p.rng;
+  const float qi = __builtin_floorf(r * p.n + 0.5f);
+  return (qi * p.rng) / p.n + p.mn;
+}
+
+// First-index argmin of sse[0..n) by ONE wave (all 64 lanes must call).
+__device__ __forceinline__ int wave_argmin_u64(const unsigned long long* sse, int n) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long best = ~0ull;
+  int bi = 0x7fffffff;
+  for (int c = lane; c < n; c += 64) {
+    const unsigned long long v = sse[c];
+    if (v < best) { best = v; bi = c; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long ov = __shfl_xor(best, off);
+    const int oi = __shfl_xor(bi, off);
+    if (ov < best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  return bi;
+}
+
+// ---------------------------------------------------------------------------
+// The 200-candidate SSE sweep over one chunk of quads held in LDS.
+// Lane -> candidate mapping per 64-candidate group g: cnt = min(64, n-64g)
+// candidates over p2 = pow2ceil(cnt) lanes, S = 64/p2 interleaved quad streams.
+// Each lane accumulates its canonical fixed-point SSE and the group's S streams
+// are folded with xor-shuffles; lanes of stream 0 add into sse[] atomically.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void sse_sweep(const float4* __restrict__ xs, int nqc, float mx, int K, int ncand,
+                                          int bits, unsigned long long* __restrict__ sse) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const int q = 1 << (bits - 1);
+  const float qlo = (float)(-q), qhi = (float)(q - 1);
+  const float den = (float)(2 * q - 1);
+  // near-half-integer window for the reciprocal fast path: > 3 ulp of |y| <= q+1
+  const float delta = (float)(q + 1) * 0x1p-21f;
+  const int ngroups = (ncand + 63) >> 6;
+  for (int g = wave; g < ngroups; g += nwaves) {
+    const int cnt = min(64, ncand - 64 * g);
+    int lg = 0;
+    while ((1 << lg) < cnt) ++lg;
+    const int p2 = 1 << lg;
+    const int S = 64 >> lg;
+    const int csub = lane & (p2 - 1);
+    const int stream = lane >> lg;
+    const bool active = csub < cnt;
+    const int c = 64 * g + (active ? csub : 0);
+    const float t = cand_t(mx, c, ncand);
+    const float s = (2.0f * t) / den;
+    const float rcp = 1.0f / s;
+    unsigned long long acc = 0;
+    for (int k = stream; k < nqc; k += S) {
+      const float4 v = xs[k];
+      float y0 = v.x * rcp, y1 = v.y * rcp, y2 = v.z * rcp, y3 = v.w * rcp;
+      float q0 = __builtin_rintf(y0), q1 = __builtin_rintf(y1), q2 = __builtin_rintf(y2), q3 = __builtin_rintf(y3);
+      // distance of each y to the nearest half-integer; one compare per quad
+      const float e0 = __builtin_fabsf(__builtin_fabsf(y0 - q0) - 0.5f);
+      const float e1 = __builtin_fabsf(__builtin_fabsf(y1 - q1) - 0.5f);
+      const float e2 = __builtin_fabsf(__builtin_fabsf(y2 - q2) - 0.5f);
+      const float e3 = __builtin_fabsf(__builtin_fabsf(y3 - q3) - 0.5f);
+      const bool nb = __builtin_fminf(__builtin_fminf(e0, e1), __builtin_fminf(e2, e3)) < delta;
+      if (__builtin_expect(nb, 0)) {   // rare: decide the rounding with the exact IEEE quotient
+        q0 = __builtin_rintf(v.x / s); q1 = __builtin_rintf(v.y / s);
+        q2 = __builtin_rintf(v.z / s); q3 = __builtin_rintf(v.w / s);
+      }
+      q0 = __builtin_amdgcn_fmed3f(q0, qlo, qhi);
+      q1 = __builtin_amdgcn_fmed3f(q1, qlo, qhi);
+      q2 = __builtin_amdgcn_fmed3f(q2, qlo, qhi);
+      q3 = __builtin_amdgcn_fmed3f(q3, qlo, qhi);
+      const float d0 = v.x - q0 * s, d1 = v.y - q1 * s, d2 = v.z - q2 * s, d3 = v.w - q3 * s;
+      const float gq = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      acc += to_fixed(gq, K);
+    }
+    for (int off = p2; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
+    if (active && stream == 0) atomicAdd(&sse[64 * g + csub], acc);
+  }
+}
+
+// Block-level reductions -----------------------------------------------------
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, off));
+  return v;
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off));
+  return v;
+}
+
+// Resolve the quantization parameters of a job/problem inside a block.
+__device__ __forceinline__ QParams block_qparams(int scheme, int bits, const unsigned* stat,
+                                                 const unsigned long long* sse, int ncand, int has_kw,
+                                                 float kw_min, float kw_max) {
+  __shared__ int s_idx;
+  const unsigned ab = stat[0];
+  const bool has_nan = ab > 0x7F800000u;
+  if (scheme == kMse) {
+    const float mx = __uint_as_float(ab);
+    if (mse_degenerate(mx)) return qparams_mse(bits, __builtin_nanf(""));
+    if (threadIdx.x < 64) {
+      const int idx = wave_argmin_u64(sse, ncand);
+      if (threadIdx.x == 0) s_idx = idx;
+    }
+    __syncthreads();
+    return qparams_mse(bits, cand_t(mx, s_idx, ncand));
+  }
+  return qparams_stats(scheme, bits, dec_ord(stat[1]), dec_ord(stat[2]), has_nan ? 1 : 0, has_kw, kw_min, kw_max);
+}
+
+}  // namespace admmq

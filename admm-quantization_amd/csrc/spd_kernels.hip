@@ -1,0 +1,224 @@
+// M = (G + rho I)^-1 once per admm_iteration call (replaces torch.linalg.cholesky +
+// torch.cholesky_solve of source/admm.py:54,56 by an explicit inverse so that every
+// inner iteration is one GEMM). Computed in fp64 and rounded once to fp32.
+//
+// 32 x 32 blocked, batched over problems, fp64 VALU:
+//   for k:  k_chol_panel(k)   factor A_kk in LDS (-> D64); L_ik = A_ik L_kk^-T (i > k)
+//           k_chol_update(k)  A_ij -= L_ik L_jk^T                       (k < j <= i)
+//   for i:  k_linv_row(i)     Linv_ij = -Linv_ii sum_{t=j}^{i-1} L_it Linv_tj
+//   once:   k_minv            M_ij = sum_{t>=i} Linv_ti^T Linv_tj  (fp32, symmetric,
+//                              zero outside R x R)
+// A non-positive pivot sets flags[2] (the reference raises torch.linalg.LinAlgError).
+#include "admmq_internal.h"
+
+namespace admmq {
+
+constexpr int NB = 32;
+constexpr int LS = NB + 1;  // LDS row stride (doubles) to spread banks
+
+__device__ __forceinline__ void load_block(double* dst, const double* A, int ldm, int bi, int bj) {
+  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
+    const int r = t >> 5, c = t & 31;
+    dst[r * LS + c] = A[(size_t)(bi * NB + r) * ldm + bj * NB + c];
+  }
+}
+__device__ __forceinline__ void store_block(double* A, int ldm, int bi, int bj, const double* src) {
+  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
+    const int r = t >> 5, c = t & 31;
+    A[(size_t)(bi * NB + r) * ldm + bj * NB + c] = src[r * LS + c];
+  }
+}
+
+// In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed.
+__device__ void chol32(double* a, int* err) {
+  for (int c = 0; c < NB; ++c) {
+    if (threadIdx.x == 0) {
+      const double d = a[c * LS + c];
+      if (!(d > 0.0)) *err = 1;
+      a[c * LS + c] = sqrt(d);
+    }
+    __syncthreads();
+    if (threadIdx.x > c && threadIdx.x < NB) a[threadIdx.x * LS + c] /= a[c * LS + c];
+    __syncthreads();
+    const int n = NB - c - 1;
+    for (int t = threadIdx.x; t < n * n; t += blockDim.x) {
+      const int r = c + 1 + t / n, s = c + 1 + t % n;
+      if (s <= r) a[r * LS + s] -= a[r * LS + c] * a[s * LS + c];
+    }
+    __syncthreads();
+  }
+  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
+    const int r = t >> 5, c = t & 31;
+    if (c > r) a[r * LS + c] = 0.0;
+  }
+  __syncthreads();
+}
+
+// Inverse of a lower-triangular 32x32 block: column c by thread c.
+__device__ void trinv32(const double* l, double* x) {
+  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) x[(t >> 5) * LS + (t & 31)] = 0.0;
+  __syncthreads();
+  if (threadIdx.x < NB) {
+    const int c = threadIdx.x;
+    x[c * LS + c] = 1.0 / l[c * LS + c];
+    for (int r = c + 1; r < NB; ++r) {
+      double s = 0.0;
+      for (int t = c; t < r; ++t) s += l[r * LS + t] * x[t * LS + c];
+      x[r * LS + c] = -s / l[r * LS + r];
+    }
+  }
+  __syncthreads();
+}
+
+// acc[4] += A(rows r0..) * B^T or A * B for a 32x32x32 product; thread owns 4 outputs.
+// out(r, c) for r = tid>>3 (0..31), c = (tid&7)*4 + q
+__device__ __forceinline__ void mm_nt(const double* a, const double* b, double acc[4]) {  // a * b^T
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+  for (int t = 0; t < NB; ++t) {
+    const double av = a[r * LS + t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += av * b[(cb + q) * LS + t];
+  }
+}
+__device__ __forceinline__ void mm_nn(const double* a, const double* b, double acc[4]) {  // a * b
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+  for (int t = 0; t < NB; ++t) {
+    const double av = a[r * LS + t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += av * b[t * LS + cb + q];
+  }
+}
+__device__ __forceinline__ void mm_tn(const double* a, const double* b, double acc[4]) {  // a^T * b
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+  for (int t = 0; t < NB; ++t) {
+    const double av = a[t * LS + r];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += av * b[t * LS + cb + q];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_chol_panel(const ProbDesc* __restrict__ probs, int k) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const int i = k + blockIdx.x;
+  if (k >= p.nbk || i >= p.nbk) return;
+  __shared__ double lkk[NB * LS], x[NB * LS], aik[NB * LS];
+  __shared__ int err;
+  if (threadIdx.x == 0) err = 0;
+  load_block(lkk, p.A64, p.ldm, k, k);
+  __syncthreads();
+  chol32(lkk, &err);
+  if (i == k) {   // siblings still read A_kk in this launch: L_kk goes to the diagonal store
+    if (err && threadIdx.x == 0) p.flags[2] = 1;
+    store_block(p.D64, NB, k, 0, lkk);
+    return;
+  }
+  trinv32(lkk, x);                   // x = L_kk^-1
+  load_block(aik, p.A64, p.ldm, i, k);
+  __syncthreads();
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  mm_nt(aik, x, acc);                // L_ik = A_ik * (L_kk^-1)^T
+  __syncthreads();
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) aik[r * LS + cb + q] = acc[q];
+  __syncthreads();
+  store_block(p.A64, p.ldm, i, k, aik);
+}
+
+__global__ __launch_bounds__(256) void k_chol_update(const ProbDesc* __restrict__ probs, int k) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const int n = p.nbk - k - 1;
+  if (n <= 0) return;
+  const int q = blockIdx.x;
+  if (q >= n * (n + 1) / 2) return;
+  // q -> (ii, jj) with 0 <= jj <= ii < n, row-major lower triangle
+  int ii = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  while ((ii + 1) * (ii + 2) / 2 <= q) ++ii;
+  while (ii * (ii + 1) / 2 > q) --ii;
+  const int jj = q - ii * (ii + 1) / 2;
+  const int i = k + 1 + ii, j = k + 1 + jj;
+  __shared__ double li[NB * LS], lj[NB * LS];
+  load_block(li, p.A64, p.ldm, i, k);
+  load_block(lj, p.A64, p.ldm, j, k);
+  __syncthreads();
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  mm_nt(li, lj, acc);
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+  double* dst = p.A64 + (size_t)(i * NB + r) * p.ldm + j * NB + cb;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dst[t] -= acc[t];
+}
+
+__global__ __launch_bounds__(256) void k_linv_row(const ProbDesc* __restrict__ probs, int i) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const int j = blockIdx.x;
+  if (i >= p.nbk || j > i) return;
+  __shared__ double lii[NB * LS], xi[NB * LS], ta[NB * LS], tb[NB * LS];
+  load_block(lii, p.D64, NB, i, 0);
+  __syncthreads();
+  trinv32(lii, xi);
+  if (j == i) {
+    store_block(p.L64, p.ldm, i, i, xi);
+    return;
+  }
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = j; t < i; ++t) {
+    load_block(ta, p.A64, p.ldm, i, t);   // L_it
+    load_block(tb, p.L64, p.ldm, t, j);   // Linv_tj
+    __syncthreads();
+    mm_nn(ta, tb, acc);
+    __syncthreads();
+  }
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ta[r * LS + cb + q] = acc[q];
+  __syncthreads();
+  double out[4] = {0.0, 0.0, 0.0, 0.0};
+  mm_nn(xi, ta, out);                     // Linv_ii * S
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tb[r * LS + cb + q] = -out[q];
+  __syncthreads();
+  store_block(p.L64, p.ldm, i, j, tb);
+}
+
+__global__ __launch_bounds__(256) void k_minv(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const int q = blockIdx.x;
+  const int n = p.nbk;
+  if (q >= n * (n + 1) / 2) return;
+  int i = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= q) ++i;
+  while (i * (i + 1) / 2 > q) --i;
+  const int j = q - i * (i + 1) / 2;      // j <= i
+  __shared__ double ta[NB * LS], tb[NB * LS];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = i; t < n; ++t) {
+    load_block(ta, p.L64, p.ldm, t, i);   // Linv_ti
+    load_block(tb, p.L64, p.ldm, t, j);   // Linv_tj
+    __syncthreads();
+    mm_tn(ta, tb, acc);
+    __syncthreads();
+  }
+  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 4;
+  const int gr = i * NB + r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int gc = j * NB + cb + t;
+    const float v = (gr < p.R && gc < p.R) ? (float)acc[t] : 0.f;
+    p.M[(size_t)gr * p.ldm + gc] = v;
+    p.M[(size_t)gc * p.ldm + gr] = v;
+  }
+}
+
+void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s) {
+  for (int k = 0; k < maxnbk; ++k) {
+    hipLaunchKernelGGL(k_chol_panel, dim3(maxnbk - k, nprob), dim3(256), 0, s, d, k);
+    const int n = maxnbk - k - 1;
+    if (n > 0) hipLaunchKernelGGL(k_chol_update, dim3(n * (n + 1) / 2, nprob), dim3(256), 0, s, d, k);
+  }
+  for (int i = 0; i < maxnbk; ++i) hipLaunchKernelGGL(k_linv_row, dim3(i + 1, nprob), dim3(256), 0, s, d, i);
+  hipLaunchKernelGGL(k_minv, dim3(maxnbk * (maxnbk + 1) / 2, nprob), dim3(256), 0, s, d);
+}
+
+}  // namespace admmq

@@ -1,0 +1,110 @@
+/*
+ * libadmmq — MI355X-native ADMM quantized tensor-factorization hot path (C ABI).
+ *
+ * Every entry point is stream-ordered on the caller's HIP stream (`stream` is a
+ * hipStream_t passed as void*), takes plain device pointers to row-major float32
+ * buffers, uses only caller-owned workspace, and returns an int32 status
+ * (ADMMQ_OK = 0). No entry point allocates, frees or synchronises.
+ *
+ * Reference interfaces replaced (KamikaziZen/admm-quantization @ 2024_10_08):
+ *   admmq_admm_prepare + admmq_admm_run  <- source/admm.py:51-67  admm_iteration(H,U,F,G,max_iter,eps,bits,qscheme)
+ *                                           (batched over independent (layer, mode) problems)
+ *   admmq_quantize_batched               <- source/quantization.py:69-115  quantize_tensor(tensor,bits,qscheme,**kw)
+ *                                           incl. quantize_tensor_mse :118-144, min_max_quantize :48-66
+ *   admmq_mse_sse_table                  <- source/quantization.py:129-141 (the candidate search, exposed
+ *                                           for parity tests: canonical fixed-point SSE per candidate)
+ */
+#ifndef ADMMQ_H_
+#define ADMMQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADMMQ_OK 0
+#define ADMMQ_ERR_ARG (-1)
+#define ADMMQ_ERR_HIP (-2)
+#define ADMMQ_ERR_WORKSPACE (-3)
+#define ADMMQ_ERR_SCHEME (-4)
+
+/* qscheme codes (names as in source/quantization.py:91-115) */
+#define ADMMQ_TENSOR_MSEMINMAX_SYMMETRIC 0
+#define ADMMQ_TENSOR_MINMAX 1
+#define ADMMQ_TENSOR_SYMMETRIC 2
+#define ADMMQ_TENSOR_AFFINE 3
+
+/* One ADMM problem: one factor update  H <- argmin ||F - H G|| s.t. H quantized.
+ * F, H0, H_out, U: I x R; G: R x R (symmetric PSD). U is read and overwritten
+ * (source/admm.py:60 mutates the caller's U in place); H0 is never written. */
+typedef struct admmq_problem {
+  const float* F;
+  const float* G;
+  const float* H0;
+  float* H_out;
+  float* U;
+  float* HT_out; /* optional (NULL): last iteration's H_T  (debug / parity tests) */
+  float* X_out;  /* optional (NULL): last iteration's H_T - U (the quantizer input) */
+  int32_t I;
+  int32_t R;
+} admmq_problem;
+
+/* Bytes of workspace for a batch (num_attempts: MSE candidates, 200 in the reference). */
+size_t admmq_admm_workspace_size(const admmq_problem* probs, int32_t nprob, int32_t num_attempts);
+
+/* Setup of source/admm.py:52-54 for every problem: rho = tr(G)/R, M = (G + rho I)^-1
+ * (fp64 blocked Cholesky, rounded to fp32), padded copies of F/H0/U and the first
+ * right-hand side. Must precede admmq_admm_run on the same workspace. */
+int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
+/* The loop of source/admm.py:55-65: max_iter-1 iterations of {solve, quantize,
+ * dual update, residual test} per problem, with the per-problem early exit when
+ * r < eps and s < eps. Writes H_out and U. info (device int32[nprob*4], may be
+ * NULL) receives {iterations run, converged, spd_error, 0} per problem. */
+int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
+                       int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
+                       int32_t* info, void* stream);
+
+/* prepare + run. */
+int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
+                                     int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,
+                                     size_t workspace_bytes, int32_t* info, void* stream);
+
+/* One quantize_tensor call: x viewed as (rows, cols) with cols the last dimension. */
+typedef struct admmq_qtensor {
+  const float* x;
+  float* y;
+  int64_t rows;
+  int64_t cols;
+  float tmin; /* tensor_affine kwargs (source/quantization.py:98-101) when has_minmax */
+  float tmax;
+  int32_t has_minmax;
+  int32_t reserved;
+} admmq_qtensor;
+
+size_t admmq_quantize_workspace_size(const admmq_qtensor* t, int32_t n, int32_t num_attempts);
+int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, int32_t qscheme, int32_t num_attempts,
+                               void* workspace, size_t workspace_bytes, void* stream);
+
+/* Canonical SSE table of the MSE-minmax search for one tensor (sse_out: device uint64[num_attempts]). */
+int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,
+                            uint64_t* sse_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Optional HIP-event timing of every launch class issued by admmq_admm_prepare/run on
+ * this thread between begin and end: class 0 GEMM (solve), 1 MSE candidate sweep,
+ * 2 projection/dual update, 3 whole prepare phase. end() synchronises on the last event
+ * and returns summed milliseconds and launch counts per class (arrays of 4). */
+int32_t admmq_profile_begin(int32_t max_launches);
+int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class);
+
+/* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
+int32_t admmq_version(void);
+const char* admmq_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADMMQ_H_ */

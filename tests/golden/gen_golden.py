@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the reference implementation (survey container only).
+
+Run:  python3 -B tests/golden/gen_golden.py [--reference /root/reference] [--skip-band]
+
+The reference (``/root/reference``, read-only) is imported with ``tensorly`` and
+``musco`` stubbed (they are only used by the ``parafac``/``parafac-epc`` init
+paths, which cannot run offline). Nothing is written into the reference tree
+(``sys.dont_write_bytecode``). Only data is written: inputs are regenerated from
+numpy seeds, outputs are stored as arrays or SHA-256 digests, under
+``tests/golden/``.
+
+Fixture families:
+  F1  quantizer KATs  -> f1_quant.npz + f1_quant.json
+  F2  few-step ADMM   -> f2_admm.npz
+  F3  short ALS loop  -> f3_als.npz
+  F4  long-horizon objective band over torch thread counts -> f4_band.json
+  F5  candidate grids (torch.linspace) -> f5_linspace.npz
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "admm-quantization_amd"))
+sys.path.insert(0, HERE)
+from admmq import synthetic  # noqa: E402
+import golden_cases as gc  # noqa: E402
+
+
+class _Stub(types.ModuleType):
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+
+        def _raise(*a, **k):
+            raise RuntimeError(f"stubbed third-party call {self.__name__}.{name}")
+        return _raise
+
+
+def import_reference(path):
+    for m in ["tensorly", "tensorly.decomposition", "tensorly.decomposition.candecomp_parafac",
+              "tensorly.kruskal_tensor", "musco", "musco.pytorch", "musco.pytorch.compressor",
+              "musco.pytorch.compressor.decompose", "musco.pytorch.compressor.decompose.cpd",
+              "musco.pytorch.compressor.decompose.cpd.lib_anc"]:
+        sys.modules[m] = _Stub(m)
+    sys.path.insert(0, path)
+    from source import admm as ref_admm  # noqa: E402
+    from source import quantization as ref_quant  # noqa: E402
+    return ref_admm, ref_quant
+
+
+def sha(a: np.ndarray) -> str:
+    """SHA-256 of the float32 bytes with every NaN canonicalised to 0x7fc00000
+    (NaN sign/payload is not meaningful across CPU/GPU; signed zeros are kept)."""
+    return gc.canonical_sha(a)
+
+
+def gen_f1(ref_quant, out):
+    meta = []
+    arrays = {}
+    for case in gc.f1_cases():
+        x = gc.f1_input(case)
+        kw = {}
+        if case.get("num_attempts") is not None:
+            kw["num_attempts"] = case["num_attempts"]
+        try:
+            y = ref_quant.quantize_tensor(torch.from_numpy(x.copy()), bits=case["bits"],
+                                          qscheme=case["qscheme"], **kw)
+            y = y.numpy().astype(np.float32)
+            rec = dict(case, error=None, sha=sha(y), out_dtype=str(y.dtype))
+            if case["store"]:
+                arrays[case["id"]] = y
+        except Exception as e:  # error behaviour is part of the contract
+            rec = dict(case, error=type(e).__name__, sha=None)
+        meta.append(rec)
+    np.savez_compressed(os.path.join(out, "f1_quant.npz"), **arrays)
+    with open(os.path.join(out, "f1_quant.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(f"F1: {len(meta)} cases, {len(arrays)} stored arrays")
+
+
+def gen_f5(out):
+    arrays = {}
+    rng = np.random.default_rng(5)
+    mxs = np.concatenate([np.abs(rng.standard_normal(48)) * 10.0 ** rng.integers(-4, 3, 48),
+                          np.array([1.0, 0.5, 3.0, 1e-3, 123.456, 7e-5, 2.0 ** -20, 65504.0,
+                                    0.1, 0.3, 1.7, 2.9, 4.2, 9.99, 0.0123, 5e-2])]).astype(np.float32)
+    arrays["mx"] = mxs
+    for n in (200, 1000, 50, 2, 3, 1):
+        grids = np.stack([torch.linspace(0.2 * float(m), 1.2 * float(m), n).numpy() for m in mxs])
+        arrays[f"grid_{n}"] = grids.astype(np.float32)
+    np.savez_compressed(os.path.join(out, "f5_linspace.npz"), **arrays)
+    print("F5: linspace grids for", len(mxs), "values")
+
+
+def mttkrp_ref(W, A, B, C, mode):
+    # scripts/factorize.py:215-237 (Gram∘Gram and MTTKRP per mode)
+    if mode == 0:
+        return B.T @ B * (C.T @ C), torch.einsum('abc,cr,br->ar', W, C, B)
+    if mode == 1:
+        return A.T @ A * (C.T @ C), torch.einsum('abc,cr,ar->br', W, C, A)
+    return A.T @ A * (B.T @ B), torch.einsum('abc,br,ar->cr', W, B, A)
+
+
+def gen_f2(ref_admm, out):
+    arrays = {}
+    eps = 1e-8
+    # 3-way: resnet18 layer1.0.conv1 (64,64,9), R=134, all three modes from the seed-42 init.
+    li, spec = synthetic.find_layer("resnet18", "layer1.0.conv1")
+    W = torch.from_numpy(synthetic.layer_weight(spec, li))
+    R = spec.rank(2.0)
+    A, B, C = ref_admm.init_factors(W, rank=R, init="random", device="cpu", seed=42)
+    arrays["l1_W"] = W.numpy()
+    for nm, t in zip("ABC", (A, B, C)):
+        arrays[f"l1_{nm}"] = t.numpy()
+    for mode in range(3):
+        G, F = mttkrp_ref(W, A, B, C, mode)
+        H0 = (A, B, C)[mode]
+        arrays[f"l1_m{mode}_G"] = G.numpy()
+        arrays[f"l1_m{mode}_F"] = F.numpy()
+        for qs in gc.F2_SCHEMES if mode == 0 else ["tensor_mseminmax_symmetric"]:
+            for mi in (2, 3, 6):
+                U = torch.zeros_like(H0)
+                H, U2 = ref_admm.admm_iteration(H0.clone(), U, F, G, max_iter=mi, eps=eps, bits=4, qscheme=qs)
+                arrays[f"l1_m{mode}_{qs}_it{mi}_H"] = H.numpy()
+                arrays[f"l1_m{mode}_{qs}_it{mi}_U"] = U2.numpy()
+    # 2-way (64,48): F = W B, G = B^T B (scripts/factorize.py:276-277), R = int(numel/sum/2) = 13
+    rng = np.random.default_rng(77)
+    W2 = torch.from_numpy((rng.standard_normal((64, 48)) * 0.1).astype(np.float32))
+    R2 = int(W2.numel() / sum(W2.shape) / 2.0)
+    A2, B2 = ref_admm.init_factors(W2, rank=R2, init="random", device="cpu", seed=42)
+    arrays["w2_W"], arrays["w2_A"], arrays["w2_B"] = W2.numpy(), A2.numpy(), B2.numpy()
+    G2, F2 = B2.T @ B2, W2 @ B2
+    arrays["w2_G"], arrays["w2_F"] = G2.numpy(), F2.numpy()
+    for mi in (2, 3, 6):
+        H, U2 = ref_admm.admm_iteration(A2.clone(), torch.zeros_like(A2), F2, G2, max_iter=mi, eps=eps,
+                                        bits=4, qscheme="tensor_mseminmax_symmetric")
+        arrays[f"w2_it{mi}_H"], arrays[f"w2_it{mi}_U"] = H.numpy(), U2.numpy()
+    # init_factors 'svd' (source/admm.py:29-35) on the 2-way and 3-way tensors
+    for nm, T, r in (("l1", W, R), ("w2", W2, R2)):
+        fs = ref_admm.init_factors(T, rank=r, init="svd", device="cpu", seed=42)
+        for m, f in enumerate(fs):
+            arrays[f"{nm}_svd_m{m}"] = f.numpy()
+    np.savez_compressed(os.path.join(out, "f2_admm.npz"), **arrays)
+    print("F2:", len(arrays), "arrays")
+
+
+def als_reference(ref_admm, ref_quant, W, R, max_iter_als, max_iter_admm, bits=4,
+                  qscheme="tensor_mseminmax_symmetric", seed=42):
+    """Restatement of scripts/factorize.py:178-266 (3-way) / 269-310 (2-way) that
+    calls the reference's own admm_iteration / quantize_tensor / squared_relative_diff."""
+    eps, tol = 1e-8, 1e-5
+    sq = ref_admm.squared_relative_diff
+    factors = ref_admm.init_factors(W, rank=R, init="random", device="cpu", seed=seed)
+    loss, lossq = [], []
+    if W.ndim == 3:
+        A, B, C = factors
+        UA, UB, UC = (torch.zeros_like(t) for t in (A, B, C))
+        for _ in range(max_iter_als):
+            G, F = B.T @ B * (C.T @ C), torch.einsum('abc,cr,br->ar', W, C, B)
+            A, UA = ref_admm.admm_iteration(A, UA, F, G, max_iter=max_iter_admm, eps=eps, bits=bits, qscheme=qscheme)
+            Aq = ref_quant.quantize_tensor(A, qscheme=qscheme, bits=bits)
+            G, F = A.T @ A * (C.T @ C), torch.einsum('abc,cr,ar->br', W, C, A)
+            B, UB = ref_admm.admm_iteration(B, UB, F, G, max_iter=max_iter_admm, eps=eps, bits=bits, qscheme=qscheme)
+            Bq = ref_quant.quantize_tensor(B, qscheme=qscheme, bits=bits)
+            G, F = A.T @ A * (B.T @ B), torch.einsum('abc,br,ar->cr', W, B, A)
+            C, UC = ref_admm.admm_iteration(C, UC, F, G, max_iter=max_iter_admm, eps=eps, bits=bits, qscheme=qscheme)
+            Cq = ref_quant.quantize_tensor(C, qscheme=qscheme, bits=bits)
+            loss.append(sq(W, torch.einsum('ir,jr,kr->ijk', A, B, C)))
+            lossq.append(sq(W, torch.einsum('ir,jr,kr->ijk', Aq, Bq, Cq)))
+            if len(loss) > 1 and abs(loss[-2] - loss[-1]) < tol:
+                break
+            if len(loss) > 10 and loss[-1] - loss[-5] > 1e-3:
+                break
+        return [A, B, C], [Aq, Bq, Cq], loss, lossq
+    A, B = factors
+    UA, UB = torch.zeros_like(A), torch.zeros_like(B)
+    for _ in range(max_iter_als):
+        A, UA = ref_admm.admm_iteration(A, UA, W @ B, B.T @ B, max_iter=max_iter_admm, eps=eps, bits=bits, qscheme=qscheme)
+        Aq = ref_quant.quantize_tensor(A, qscheme=qscheme, bits=bits)
+        B, UB = ref_admm.admm_iteration(B, UB, W.T @ A, A.T @ A, max_iter=max_iter_admm, eps=eps, bits=bits, qscheme=qscheme)
+        Bq = ref_quant.quantize_tensor(B, qscheme=qscheme, bits=bits)
+        loss.append(sq(W, A @ B.T))
+        lossq.append(sq(W, Aq @ Bq.T))
+        if len(loss) > 1 and abs(loss[-2] - loss[-1]) < tol:
+            break
+        if len(loss) > 10 and loss[-1] - loss[-10] > 1e-3:
+            break
+    return [A, B], [Aq, Bq], loss, lossq
+
+
+def gen_f3(ref_admm, ref_quant, out):
+    arrays = {}
+    li, spec = synthetic.find_layer("resnet18", "layer1.0.conv1")
+    W = torch.from_numpy(synthetic.layer_weight(spec, li))
+    fs, fq, loss, lossq = als_reference(ref_admm, ref_quant, W, spec.rank(2.0), 2, 3)
+    for m in range(3):
+        arrays[f"l1_f{m}"], arrays[f"l1_q{m}"] = fs[m].numpy(), fq[m].numpy()
+    arrays["l1_loss"], arrays["l1_lossq"] = np.array(loss), np.array(lossq)
+    rng = np.random.default_rng(77)
+    W2 = torch.from_numpy((rng.standard_normal((64, 48)) * 0.1).astype(np.float32))
+    fs, fq, loss, lossq = als_reference(ref_admm, ref_quant, W2, 13, 3, 4)
+    for m in range(2):
+        arrays[f"w2_f{m}"], arrays[f"w2_q{m}"] = fs[m].numpy(), fq[m].numpy()
+    arrays["w2_loss"], arrays["w2_lossq"] = np.array(loss), np.array(lossq)
+    np.savez_compressed(os.path.join(out, "f3_als.npz"), **arrays)
+    print("F3: done", loss, lossq)
+
+
+def gen_f4(ref_admm, ref_quant, out):
+    li, spec = synthetic.find_layer("resnet18", "layer1.0.conv1")
+    W = torch.from_numpy(synthetic.layer_weight(spec, li))
+    res = {}
+    for th in (1, 2, 4, 8):
+        torch.set_num_threads(th)
+        _, _, loss, lossq = als_reference(ref_admm, ref_quant, W, spec.rank(2.0), 20, 20)
+        res[str(th)] = {"loss": loss, "lossq": lossq}
+        print(f"F4 threads={th}: rec {loss[-1]:.6f} quant {lossq[-1]:.6f} sweeps {len(loss)}")
+    torch.set_num_threads(8)
+    with open(os.path.join(out, "f4_band.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--skip-band", action="store_true")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    torch.set_num_threads(8)
+    ref_admm, ref_quant = import_reference(a.reference)
+    only = set(a.only.split(",")) if a.only else {"f1", "f2", "f3", "f4", "f5"}
+    if "f5" in only:
+        gen_f5(HERE)
+    if "f1" in only:
+        gen_f1(ref_quant, HERE)
+    if "f2" in only:
+        gen_f2(ref_admm, HERE)
+    if "f3" in only:
+        gen_f3(ref_admm, ref_quant, HERE)
+    if "f4" in only and not a.skip_band:
+        gen_f4(ref_admm, ref_quant, HERE)
+    meta = {"torch": torch.__version__, "numpy": np.__version__, "threads": 8,
+            "reference": "KamikaziZen/admm-quantization @ 2024_10_08",
+            "generator": "tests/golden/gen_golden.py"}
+    with open(os.path.join(HERE, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

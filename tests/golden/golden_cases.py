@@ -1,0 +1,103 @@
+"""Case tables shared by the golden generator and the parity tests.
+
+Inputs are regenerated from numpy seeds (PCG64 is platform-independent), so the
+fixtures only hold reference *outputs* (arrays for small cases, SHA-256 digests
+for the rest).
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+F1_SHAPES = [(9, 134), (64, 134), (9, 1141), (128, 278)]
+F1_SCALES = [1e-3, 0.05, 1.0]
+F1_BITS = [2, 3, 4, 8]
+F1_SCHEMES = ["tensor_mseminmax_symmetric", "tensor_minmax", "tensor_symmetric", "tensor_affine"]
+F2_SCHEMES = ["tensor_mseminmax_symmetric", "tensor_minmax", "tensor_symmetric", "tensor_affine"]
+
+
+def f1_cases():
+    cases = []
+    seed = 0
+    for shape in F1_SHAPES:
+        for scale in F1_SCALES:
+            for bits in F1_BITS:
+                for qs in F1_SCHEMES:
+                    seed += 1
+                    cases.append(dict(id=f"c{seed:04d}", kind="randn", shape=list(shape), scale=scale,
+                                      bits=bits, qscheme=qs, seed=seed, num_attempts=None,
+                                      store=shape == (9, 134)))
+    # large MSE-minmax shapes (digest only): layer4-sized factor, Llama-ish wide row
+    for shape, bits in (((512, 1141), 4), ((256, 566), 4), ((64, 1492), 2)):
+        seed += 1
+        cases.append(dict(id=f"c{seed:04d}", kind="randn", shape=list(shape), scale=0.3, bits=bits,
+                          qscheme="tensor_mseminmax_symmetric", seed=seed, num_attempts=None, store=False))
+    # num_attempts variants (scripts/custom_benchmark.py:195 uses 1000)
+    for na in (1000, 50, 7, 2, 1):
+        seed += 1
+        cases.append(dict(id=f"c{seed:04d}", kind="randn", shape=[64, 134], scale=1.0, bits=4,
+                          qscheme="tensor_mseminmax_symmetric", seed=seed, num_attempts=na, store=True))
+    # edge cases
+    edge = [
+        ("zeros", [9, 134]), ("const", [3, 5]), ("one", [1, 1]), ("vec", [7]), ("cube", [2, 3, 4]),
+        ("outlier", [16, 40]), ("negative", [8, 13]), ("ints", [6, 20]), ("nan", [4, 9]), ("inf", [4, 9]),
+        ("tiny", [5, 17]), ("halfgrid", [8, 33]), ("bits1", [9, 134]),
+    ]
+    for kind, shape in edge:
+        for qs in F1_SCHEMES:
+            seed += 1
+            cases.append(dict(id=f"c{seed:04d}", kind=kind, shape=shape, scale=1.0,
+                              bits=1 if kind == "bits1" else 4, qscheme=qs, seed=seed,
+                              num_attempts=None, store=True))
+    # error behaviour (source/quantization.py:29-41, 114-115)
+    for qs in ("channel_symmetric", "channel_affine", "tensor_log", "bogus"):
+        seed += 1
+        cases.append(dict(id=f"c{seed:04d}", kind="randn", shape=[4, 6], scale=1.0, bits=4, qscheme=qs,
+                          seed=seed, num_attempts=None, store=False))
+    return cases
+
+
+def f1_input(case) -> np.ndarray:
+    shape = tuple(case["shape"])
+    rng = np.random.default_rng(case["seed"])
+    kind = case["kind"]
+    if kind in ("randn", "bits1"):
+        x = rng.standard_normal(shape) * case["scale"]
+    elif kind == "zeros":
+        x = np.zeros(shape)
+    elif kind == "const":
+        x = np.full(shape, 0.5)
+    elif kind == "one":
+        x = np.full(shape, -1.25)
+    elif kind in ("vec", "cube"):
+        x = rng.standard_normal(shape)
+    elif kind == "outlier":
+        x = rng.standard_normal(shape) * 0.01
+        x.flat[17] = 3.0
+    elif kind == "negative":
+        x = -np.abs(rng.standard_normal(shape)) - 0.1
+    elif kind == "ints":
+        x = rng.integers(-9, 9, shape).astype(np.float64)
+    elif kind == "nan":
+        x = rng.standard_normal(shape)
+        x.flat[3] = np.nan
+    elif kind == "inf":
+        x = rng.standard_normal(shape)
+        x.flat[5] = np.inf
+    elif kind == "tiny":
+        x = rng.standard_normal(shape) * 1e-30
+    elif kind == "halfgrid":
+        # values on k/2 multiples of a candidate-like scale: exercises round-half-even
+        x = rng.integers(-16, 16, shape) * 0.5 * (2.0 * 0.6 / 15.0)
+    else:
+        raise ValueError(kind)
+    return x.astype(np.float32)
+
+
+def canonical_sha(a) -> str:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float32)).copy()
+    a[np.isnan(a)] = np.float32(np.nan)
+    u = a.view(np.uint32)
+    u[np.isnan(a)] = np.uint32(0x7FC00000)
+    return hashlib.sha256(u.tobytes()).hexdigest()

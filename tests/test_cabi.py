@@ -1,0 +1,83 @@
+"""CPU tests of the C-ABI library: it loads without a GPU, exports every symbol that
+include/admmq.h declares, and its host-side planner answers (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "admmq.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from admmq import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libadmmq.so is not built: run __graft_entry__.build()")
+    return _lib.load()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(admmq_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("admmq_admm_prepare", "admmq_admm_run", "admmq_quantize_batched", "admmq_mse_sse_table"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert missing == []
+
+
+def test_struct_layouts_match_header():
+    from admmq import _lib
+    assert ctypes.sizeof(_lib.AdmmProblem) == 7 * 8 + 2 * 4
+    assert ctypes.sizeof(_lib.QTensor) == 2 * 8 + 2 * 8 + 2 * 4 + 2 * 4
+
+
+def test_version_and_error_text(lib):
+    assert lib.admmq_version() >= 100
+    assert isinstance(lib.admmq_last_error(), bytes)
+
+
+def test_workspace_planner(lib):
+    from admmq import _lib
+    p = _lib.AdmmProblem(0, 0, 0, 0, 0, 0, 0, 64, 134)
+    arr = _lib.problems_array([p])
+    one = lib.admmq_admm_workspace_size(arr, 1, 200)
+    # Fp,H,U,P,X,HT (64 x 144 f32) + M (192^2 f32) + A64,L64 (192^2 f64) + D64 + tables
+    assert one >= 6 * 64 * 144 * 4 + 192 * 192 * 4 + 2 * 192 * 192 * 8
+    big = _lib.AdmmProblem(0, 0, 0, 0, 0, 0, 0, 512, 1141)
+    two = lib.admmq_admm_workspace_size(_lib.problems_array([p, big]), 2, 200)
+    assert two > one
+    assert lib.admmq_admm_workspace_size(arr, 0, 200) == 0          # no problems -> error (0)
+    bad = _lib.AdmmProblem(0, 0, 0, 0, 0, 0, 0, 0, 5)
+    assert lib.admmq_admm_workspace_size(_lib.problems_array([bad]), 1, 200) == 0
+    assert b"positive" in lib.admmq_last_error()
+
+
+def test_quantize_planner(lib):
+    from admmq import _lib
+    t = _lib.QTensor(0, 0, 9, 134, 0.0, 0.0, 0, 0)
+    n = lib.admmq_quantize_workspace_size(_lib.qtensor_array([t]), 1, 200)
+    assert n >= 9 * 136 * 4 + 200 * 8
+    assert lib.admmq_quantize_workspace_size(_lib.qtensor_array([t]), 1, 0) == 0
+
+
+def test_product_path_refuses_cpu_tensors():
+    import torch
+    from admmq import quantize_tensor, admm_iteration
+    x = torch.randn(4, 5)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        quantize_tensor(x, 4, "tensor_mseminmax_symmetric")
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        admm_iteration(x, torch.zeros_like(x), x, torch.eye(5), 3, 1e-8, 4, "tensor_mseminmax_symmetric")
+    with pytest.raises(TypeError):
+        quantize_tensor(x, 4, "channel_affine")
+    with pytest.raises(NotImplementedError):
+        quantize_tensor(x, 4, "tensor_log")

@@ -1,0 +1,78 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/, made by
+tests/golden/gen_golden.py from /root/reference). CPU only."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import golden_cases as gc
+from oracle import quant_oracle as qo
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _sha(a):
+    return gc.canonical_sha(a)
+
+
+def _load_f1():
+    with open(os.path.join(GOLDEN, "f1_quant.json")) as f:
+        meta = json.load(f)
+    arrays = np.load(os.path.join(GOLDEN, "f1_quant.npz"))
+    return meta, arrays
+
+
+def test_f5_candidate_grid_bit_exact():
+    z = np.load(os.path.join(GOLDEN, "f5_linspace.npz"))
+    mxs = z["mx"]
+    for n in (200, 1000, 50, 2, 3, 1):
+        ref = z[f"grid_{n}"]
+        got = np.stack([qo.candidate_grid(m, n) for m in mxs])
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), n
+
+
+def _run_case(case):
+    x = gc.f1_input(case)
+    kw = {}
+    if case.get("num_attempts") is not None:
+        kw["num_attempts"] = case["num_attempts"]
+    return qo.quantize_tensor(x, case["bits"], case["qscheme"], **kw)
+
+
+def test_f1_quantizer_kats():
+    meta, arrays = _load_f1()
+    mism = []
+    for case in meta:
+        if case["error"] is not None:
+            with pytest.raises((TypeError, NotImplementedError)):
+                _run_case(case)
+            continue
+        y = _run_case(case)
+        if _sha(y.astype(np.float32)) != case["sha"]:
+            mism.append(case["id"])
+    # Every committed KAT must agree bit-for-bit (no near-tie exemptions needed so far).
+    assert mism == [], f"{len(mism)} of {len(meta)} KATs differ: {mism[:20]}"
+
+
+def test_f1_stored_arrays_match():
+    meta, arrays = _load_f1()
+    for case in meta:
+        if case["id"] in arrays.files:
+            y = _run_case(case)
+            ref = arrays[case["id"]]
+            assert y.shape == ref.shape
+            assert np.array_equal(y.view(np.uint32), ref.view(np.uint32)) or (
+                np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
+            ), case["id"]
+
+
+def test_sse_table_is_order_independent():
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((37, 53)).astype(np.float32)
+    sse, grid, mx = qo.mse_sse_table(x, 4)
+    # permuting whole quads must not change any SSE (associative integer sums)
+    xp = x[::-1].copy()
+    sse2, _, _ = qo.mse_sse_table(xp, 4)
+    assert np.array_equal(sse, sse2)

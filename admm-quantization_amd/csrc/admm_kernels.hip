@@ -134,8 +134,8 @@ __global__ __launch_bounds__(256) void k_unpack(const ProbDesc* __restrict__ pro
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(e / p.R), c = (int)(e - (long long)r * p.R);
     const size_t o = (size_t)r * p.ld + c;
-    p.H_out[e] = p.H[o];
-    p.U_user[e] = p.U[o];
+    if (p.H_out) p.H_out[e] = p.H[o];
+    if (p.U_user) p.U_user[e] = p.U[o];
     if (p.HT_dbg) p.HT_dbg[e] = p.HT[o];
     if (p.X_dbg) p.X_dbg[e] = p.X[o];
   }

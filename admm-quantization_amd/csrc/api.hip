@@ -309,6 +309,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // descriptors carry this call's output pointers (H_out may differ from prepare's)
+  if ((rc = upload_admm(pl, s))) return rc;
   const int ntiles = (int)pl.tiles.size(), nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;

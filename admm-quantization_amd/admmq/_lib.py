@@ -56,6 +56,7 @@ def load() -> ctypes.CDLL:
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
+        "admmq_set_exhaustive_search": (I32, [I32]),
         "admmq_profile_begin": (I32, [I32]),
         "admmq_profile_end": (I32, [P, P]),
         "admmq_version": (I32, []),
@@ -105,3 +106,20 @@ def problems_array(items: Sequence[AdmmProblem]):
 
 def qtensor_array(items: Sequence[QTensor]):
     return (QTensor * len(items))(*items)
+
+
+class exhaustive_search:
+    """Context manager: evaluate every MSE candidate (the reference's 200 full passes)
+    instead of the default two-stage exact search. Results are bit-identical; used
+    for A/B timing and as a cross-check in the parity tests."""
+
+    def __init__(self, enable: bool = True):
+        self.enable = enable
+
+    def __enter__(self):
+        load().admmq_set_exhaustive_search(1 if self.enable else 0)
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_set_exhaustive_search(0)
+        return False

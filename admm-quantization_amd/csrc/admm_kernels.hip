@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void k_rho(const ProbDesc* __restrict__ probs)
     p.rho[0] = (float)tr / (float)p.R;
     p.flags[0] = 0; p.flags[1] = 0; p.flags[2] = 0; p.flags[3] = 0;
     for (int sl = 0; sl < 2; ++sl) {
-      p.stat[4 * sl + 0] = 0u; p.stat[4 * sl + 1] = 0xFFFFFFFFu; p.stat[4 * sl + 2] = 0u; p.stat[4 * sl + 3] = 0u;
+      unsigned* st = p.mv.stat + 4 * sl;
+      st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
       for (int k = 0; k < 4; ++k) p.res[4 * sl + k] = 0.0;
     }
   }
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
   const Chunk ck = chunks[blockIdx.x];
   const ProbDesc& p = probs[ck.job];
   if (p.flags[0]) return;
-  const QParams qp = block_qparams(scheme, bits, p.stat + 4 * slot, p.sse + (size_t)slot * ncand, ncand, 0, 0.f, 0.f);
+  const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);
   const float rho = p.rho[0];
   const long long total = (long long)p.I * p.ld;
   const long long e = (long long)ck.start + 4LL * threadIdx.x;
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
   }
   if (ck.start == 0 && threadIdx.x == 0) {
     p.flags[1] = iter + 1;
-    unsigned* st = p.stat + 4 * (slot ^ 1);
+    unsigned* st = p.mv.stat + 4 * (slot ^ 1);
     st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
     double* rs = p.res + 4 * (slot ^ 1);
     rs[0] = 0.0; rs[1] = 0.0; rs[2] = 0.0; rs[3] = 0.0;

@@ -7,10 +7,9 @@
 //                        symmetric, zero outside the R x R block
 //   A64, L64           : float64 [ldm x ldm] SPD factor / inverse-factor scratch
 //   D64                : float64 [ldm x 32] diagonal Cholesky blocks
-//   stat[2][4]         : per parity slot {absmax bits, min enc, max enc, 0}
-//   sse[2][ncand]      : per parity slot, canonical fixed-point SSE per candidate
 //   res[2][4]          : per parity slot, fp64 residual sums S1..S4 (source/admm.py:62-63)
 //   flags[4]           : {done, iterations, spd_error, 0}
+// and one MseView of per-slot quantizer state (below).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,6 +17,28 @@
 namespace admmq {
 
 enum QScheme { kMse = 0, kMinMax = 1, kSymmetric = 2, kAffine = 3 };
+
+constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaustive)
+constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
+
+// Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
+// `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
+// two exact stages: stage 1 accumulates per-candidate level sums h1 (sum |x| per
+// breakpoint, fixed point) / h2 (sum 2k-1 per breakpoint) and s2 = sum x^2; select
+// turns them into A(c) +- E(c) and the candidate set S; stage 2 evaluates the
+// canonical SSE only on S (sel = {nS, c*, list...}); nS == ncand means exhaustive.
+struct MseView {
+  const float* X;              // rows x ld, zero pads
+  int rows, cols, ld, qpr;     // qpr = ceil(cols/4)
+  int nq, nelem;               // quads of the valid region, rows*cols
+  unsigned* stat;              // [slot][4] {absmax bits, min enc, max enc, 0}
+  unsigned long long* sse;     // [slot][ncand] canonical fixed-point SSE
+  unsigned long long* h1;      // [slot][ncand+1]
+  unsigned long long* h2;      // [slot][ncand+1]
+  double* s2;                  // [slot]
+  int* sel;                    // [slot][2 + kMaxSel]
+  const int* done;             // early-exit flag (ADMM) or nullptr
+};
 
 struct ProbDesc {
   // caller buffers (I x R contiguous)
@@ -32,8 +53,7 @@ struct ProbDesc {
   float* Fp; float* H; float* U; float* P; float* X; float* HT;
   float* M;
   double* A64; double* L64; double* D64;   // D64: diagonal L blocks [nbk][32][32]
-  unsigned* stat;
-  unsigned long long* sse;
+  MseView mv;
   double* res;
   int* flags;
   float* rho;
@@ -47,8 +67,7 @@ struct QJob {
   const float* src;   // rows x cols contiguous (user)
   float* dst;         // rows x cols contiguous (user)
   float* Xp;          // padded copy rows x ld (workspace)
-  unsigned* stat;     // [4]
-  unsigned long long* sse;  // [ncand]
+  MseView mv;         // one slot
   int rows, cols, ld, nq;
   float tmin_kw, tmax_kw;   // affine kwargs (NaN = unset)
   int has_kw, pad_;
@@ -74,18 +93,23 @@ void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps,
                  int ncand, hipStream_t s);
-void launch_sse_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
-                     hipStream_t s);
+// two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
+void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                     int slot, hipStream_t s);
+void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
+                       hipStream_t s);
+void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                    int slot, hipStream_t s);
 void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits,
                           int qscheme, int slot, int iter, hipStream_t s);
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
 
 void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s);
-void launch_sse_q(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, hipStream_t s);
 void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
                    hipStream_t s);
 
-constexpr int kSseQuads = 512;      // quads per SSE work unit (2048 elements, 8 KiB LDS)
+constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
+constexpr int kHistElems = 4096;    // elements per stage-1 work unit
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 
 }  // namespace admmq

@@ -50,6 +50,8 @@ struct Prof {
   size_t next = 0;
 };
 static Prof g_prof;
+// A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
+static bool g_exhaustive = false;
 
 static inline void prof_mark(hipStream_t s) {
   if (!g_prof.on || g_prof.next >= g_prof.ev.size()) return;
@@ -73,15 +75,25 @@ struct Carver {
   }
 };
 
+// Per-slot quantizer search state of one job.
+static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
+  v.stat = cv.take<unsigned>(4 * (size_t)nslot);
+  v.sse = cv.take<unsigned long long>((size_t)nslot * ncand);
+  v.h1 = cv.take<unsigned long long>((size_t)nslot * (ncand + 1));
+  v.h2 = cv.take<unsigned long long>((size_t)nslot * (ncand + 1));
+  v.s2 = cv.take<double>((size_t)nslot);
+  v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
+}
+
 struct AdmmPlan {
   std::vector<ProbDesc> desc;
   std::vector<GemmTile> tiles;
-  std::vector<Chunk> sse_chunks, fin_chunks;
+  std::vector<Chunk> sse_chunks, fin_chunks, hist_chunks;
   ProbDesc* d_desc = nullptr;
   GemmTile* d_tiles = nullptr;
   Chunk* d_sse = nullptr;
   Chunk* d_fin = nullptr;
-  int32_t* d_info_tmp = nullptr;
+  Chunk* d_hist = nullptr;
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
 };
@@ -112,11 +124,12 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.A64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.L64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.D64 = cv.take<double>((size_t)d.ldm * 32);
-    d.stat = cv.take<unsigned>(8);
-    d.sse = cv.take<unsigned long long>(2 * (size_t)ncand);
     d.res = cv.take<double>(8);
     d.flags = cv.take<int>(4);
     d.rho = cv.take<float>(4);
+    carve_view(cv, d.mv, 2, ncand);
+    d.mv.X = d.X; d.mv.rows = d.I; d.mv.cols = d.R; d.mv.ld = d.ld; d.mv.qpr = (d.R + 3) / 4;
+    d.mv.nq = d.nq; d.mv.nelem = d.I * d.R; d.mv.done = d.flags;
     pl.maxIp = std::max(pl.maxIp, d.Ip); pl.maxld = std::max(pl.maxld, d.ld);
     pl.maxldm = std::max(pl.maxldm, d.ldm); pl.maxnbk = std::max(pl.maxnbk, d.nbk);
     pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
@@ -133,16 +146,19 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   }
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
+  pl.hist_chunks.clear();
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
     const long long tot = (long long)d.I * d.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.fin_chunks.push_back({i, (int)e});
+    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
   }
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
+  pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
 }
@@ -153,6 +169,7 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
   return check_hip("upload");
 }
 
@@ -170,10 +187,11 @@ __global__ void k_export_info(const ProbDesc* __restrict__ d, int n, int32_t* in
 // Standalone quantization
 struct QPlan {
   std::vector<QJob> jobs;
-  std::vector<Chunk> pack_chunks, sse_chunks;
+  std::vector<Chunk> pack_chunks, sse_chunks, hist_chunks;
   QJob* d_jobs = nullptr;
   Chunk* d_pack = nullptr;
   Chunk* d_sse = nullptr;
+  Chunk* d_hist = nullptr;
   size_t bytes = 0;
 };
 
@@ -193,42 +211,61 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
     j.nq = j.rows * (j.ld / 4);
     j.has_kw = t[i].has_minmax; j.tmin_kw = t[i].tmin; j.tmax_kw = t[i].tmax;
     j.Xp = cv.take<float>((size_t)j.rows * j.ld);
-    j.stat = cv.take<unsigned>(4);
-    j.sse = cv.take<unsigned long long>(ncand);
+    carve_view(cv, j.mv, 1, ncand);
+    j.mv.X = j.Xp; j.mv.rows = j.rows; j.mv.cols = j.cols; j.mv.ld = j.ld; j.mv.qpr = j.ld / 4;
+    j.mv.nq = j.nq; j.mv.nelem = j.rows * j.cols; j.mv.done = nullptr;
   }
   pl.pack_chunks.clear();
   pl.sse_chunks.clear();
+  pl.hist_chunks.clear();
   for (int i = 0; i < n; ++i) {
     const QJob& j = pl.jobs[i];
     const long long tot = (long long)j.rows * j.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
     for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
+    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
   }
   pl.d_jobs = cv.take<QJob>(n);
   pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
+  pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
 }
 
 __global__ void k_qinit(QJob* jobs, int n, int ncand) {
-  const QJob& j = jobs[blockIdx.x];
-  for (int c = threadIdx.x; c < ncand; c += blockDim.x) j.sse[c] = 0ull;
-  if (threadIdx.x == 0) { j.stat[0] = 0u; j.stat[1] = 0xFFFFFFFFu; j.stat[2] = 0u; j.stat[3] = 0u; }
+  const MseView& v = jobs[blockIdx.x].mv;
+  for (int c = threadIdx.x; c <= ncand; c += blockDim.x) {
+    if (c < ncand) v.sse[c] = 0ull;
+    v.h1[c] = 0ull;
+    v.h2[c] = 0ull;
+  }
+  if (threadIdx.x == 0) {
+    v.stat[0] = 0u; v.stat[1] = 0xFFFFFFFFu; v.stat[2] = 0u; v.stat[3] = 0u;
+    v.s2[0] = 0.0;
+  }
 }
 
 __global__ void k_copy_sse(const QJob* jobs, int ncand, unsigned long long* out) {
-  for (int c = threadIdx.x; c < ncand; c += blockDim.x) out[c] = jobs[0].sse[c];
+  for (int c = threadIdx.x; c < ncand; c += blockDim.x) out[c] = jobs[0].mv.sse[c];
 }
 
-static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStream_t s, bool final_pass) {
+// exhaustive: evaluate every candidate's canonical SSE (debug table / forced mode)
+static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStream_t s, bool final_pass,
+                     bool exhaustive) {
   int rc;
   if ((rc = h2d(pl.d_jobs, pl.jobs.data(), n * sizeof(QJob), s))) return rc;
   if ((rc = h2d(pl.d_pack, pl.pack_chunks.data(), pl.pack_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
   hipLaunchKernelGGL(k_qinit, dim3(n), dim3(256), 0, s, pl.d_jobs, n, ncand);
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
-  if (qscheme == kMse) launch_sse_q(pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, s);
+  if (qscheme == kMse) {
+    const bool all = exhaustive || ncand > kMaxStage1;
+    if (!all) launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    launch_mse_select(nullptr, pl.d_jobs, n, ncand, bits, 0, all ? 1 : 0, s);
+    launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
+  }
   if (final_pass) launch_qfinal(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), ncand, bits, qscheme, s);
   return check_hip("quantize");
 }
@@ -243,6 +280,11 @@ static int valid_bits(int b) { return b >= 1 && b <= 16; }
 extern "C" {
 
 int32_t admmq_version(void) { return 100; }
+
+int32_t admmq_set_exhaustive_search(int32_t enable) {
+  g_exhaustive = enable != 0;
+  return ADMMQ_OK;
+}
 
 int32_t admmq_profile_begin(int32_t max_launches) {
   if (g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling already active");
@@ -312,6 +354,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
   const int ntiles = (int)pl.tiles.size(), nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
+  const int nhist = (int)pl.hist_chunks.size();
+  const bool exhaustive = g_exhaustive || num_attempts > kMaxStage1;
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);
@@ -319,7 +363,9 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
-      launch_sse_admm(pl.d_desc, pl.d_sse, nsse, num_attempts, bits, slot, s);
+      if (!exhaustive) launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      launch_mse_select(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, exhaustive ? 1 : 0, s);
+      launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       prof_mark(s);
     }
     prof_class(2); prof_mark(s);
@@ -354,7 +400,7 @@ int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, 
   int rc = plan_quant(t, n, num_attempts, workspace, pl);
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
-  return run_quant(pl, n, bits, qscheme, num_attempts, static_cast<hipStream_t>(stream), true);
+  return run_quant(pl, n, bits, qscheme, num_attempts, static_cast<hipStream_t>(stream), true, g_exhaustive);
 }
 
 int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,
@@ -368,7 +414,7 @@ int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t 
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if ((rc = run_quant(pl, 1, bits, kMse, num_attempts, s, false))) return rc;
+  if ((rc = run_quant(pl, 1, bits, kMse, num_attempts, s, false, true))) return rc;
   hipLaunchKernelGGL(k_copy_sse, dim3(1), dim3(256), 0, s, pl.d_jobs, num_attempts,
                      reinterpret_cast<unsigned long long*>(sse_out));
   return check_hip("mse_sse_table");

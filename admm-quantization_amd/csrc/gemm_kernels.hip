@@ -36,9 +36,16 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
     if (tl.first && threadIdx.x == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
     return;
   }
-  if (tl.first) {   // this iteration's SSE accumulators start at zero
-    unsigned long long* sse = p.sse + (size_t)slot * ncand;
-    for (int c = threadIdx.x; c < ncand; c += blockDim.x) sse[c] = 0ull;
+  if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+    unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
+    unsigned long long* h1 = p.mv.h1 + (size_t)slot * (ncand + 1);
+    unsigned long long* h2 = p.mv.h2 + (size_t)slot * (ncand + 1);
+    for (int c = threadIdx.x; c <= ncand; c += blockDim.x) {
+      if (c < ncand) sse[c] = 0ull;
+      h1[c] = 0ull;
+      h2[c] = 0ull;
+    }
+    if (threadIdx.x == 0) p.mv.s2[slot] = 0.0;
   }
 
   __shared__ __attribute__((aligned(16))) float As[2][BM * LROW];
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
   if (lane == 0) { red[0][wave] = amax; red[1][wave] = mn; red[2][wave] = mxo; }
   __syncthreads();
   if (tid == 0) {
-    unsigned* st = p.stat + 4 * slot;
+    unsigned* st = p.mv.stat + 4 * slot;
     atomicMax(&st[0], max(red[0][0], red[0][1]));
     atomicMin(&st[1], min(red[1][0], red[1][1]));
     atomicMax(&st[2], max(red[2][0], red[2][1]));

@@ -1,0 +1,216 @@
+// Two-stage exact MSE-minmax search (source/quantization.py:118-144).
+//
+// The reference tries 200 clipping candidates t_c with a full pass each. Its answer
+// is the first-index argmin of the canonical SSE (oracle/quant_oracle.py). Here:
+//
+// stage 1  k_mse_hist   each element x visits only its <= 2^(bits-1) level
+//                       breakpoints: for k = 1..|q(0)|, b_k = #{c : |q(c)| >= k}
+//                       (q(c) = clamp(rint(fl(x/s_c))) is monotone in c, found with a
+//                       linear estimate + exact IEEE checks), and adds |x| (fixed point)
+//                       and 2k-1 into per-candidate suffix histograms h1/h2; plus sum x^2.
+//          k_mse_select one block per job: T1(c) = sum_{b>c} h1[b], T2(c) = sum_{b>c} h2[b]
+//                       give the exact-arithmetic SSE A(c) = S2 - 2 s T1 + s^2 T2 and a
+//                       rigorous bound E(c) on |canonical - A| (oracle/stage1_model.py);
+//                       S = {c : A - E <= min(A + E)} provably holds the argmin.
+// stage 2  k_mse_sse    canonical SSE only for c in S (|S| = 1 almost always: then the
+//                       kernel exits at once); exhaustive when |S| > kMaxSel or forced.
+#include "quant_device.h"
+
+namespace admmq {
+
+__device__ __forceinline__ const MseView& mview(const ProbDesc* d, const QJob* q, int job) {
+  return d ? d[job].mv : q[job].mv;
+}
+
+// rint(fl(a / s_c)) for a >= 0 via the reciprocal fast path + exact fallback.
+__device__ __forceinline__ int level_of(float a, int c, const float* __restrict__ s_tab,
+                                        const float* __restrict__ r_tab, float delta) {
+  const float y = a * r_tab[c];
+  float q = __builtin_rintf(y);
+  if (__builtin_fabsf(__builtin_fabsf(y - q) - 0.5f) < delta) q = __builtin_rintf(a / s_tab[c]);
+  return (int)q;
+}
+
+__global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                  const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
+  const Chunk ck = chunks[blockIdx.x];
+  const MseView& v = mview(d, qj, ck.job);
+  if (v.done && *v.done) return;
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) return;
+  __shared__ float s_tab[kMaxStage1], r_tab[kMaxStage1];
+  __shared__ unsigned long long h1[kMaxStage1 + 1];
+  __shared__ unsigned h2[kMaxStage1 + 1];
+  __shared__ double red[4];
+  const int n = ncand;
+  const int qmax = 1 << (bits - 1);
+  const float den = (float)(2 * qmax - 1);
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    const float s = (2.0f * cand_t(mx, c, n)) / den;
+    s_tab[c] = s;
+    r_tab[c] = 1.0f / s;
+  }
+  for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
+  __syncthreads();
+  const float S0 = (float)(0.2 * (double)mx);
+  const float E0 = (float)(1.2 * (double)mx);
+  const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
+  const float delta = (float)(qmax + 1) * 0x1p-21f;
+  int emx;
+  (void)__builtin_frexpf(mx, &emx);
+  const long long nterm = (long long)v.nelem * qmax;
+  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
+  const int K1 = 61 - emx - clt;
+  const long long total = (long long)v.rows * v.ld;
+  const long long end = min((long long)ck.start + kHistElems, total);
+  double s2 = 0.0;
+  for (long long e = (long long)ck.start + 4LL * threadIdx.x; e < end; e += 4LL * blockDim.x) {
+    const float4 x4 = *reinterpret_cast<const float4*>(v.X + e);
+    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = xs[j];
+      if (x == 0.f) continue;
+      s2 += (double)x * (double)x;
+      const float a = __builtin_fabsf(x);
+      const int cap = (x > 0.f) ? qmax - 1 : qmax;
+      const int k0 = min(level_of(a, 0, s_tab, r_tab, delta), cap);
+      if (k0 <= 0) continue;
+      const unsigned long long af = to_fixed(a, K1);
+      int bprev = n;
+      for (int k = 1; k <= k0; ++k) {
+        // |q(c)| >= k  <=>  t_c <~ a*den/(2k-1);  t_c ~ S0 + c*step
+        const float tau = a * den * __builtin_amdgcn_rcpf((float)(2 * k - 1));   // estimate only
+        const float ce = (tau - S0) * inv_step;
+        int b = (ce >= (float)n) ? n : (ce < 0.f ? 1 : (int)ce + 1);
+        b = min(max(b, 1), bprev);
+        while (b < n && level_of(a, b, s_tab, r_tab, delta) >= k) ++b;
+        while (b > 1 && level_of(a, b - 1, s_tab, r_tab, delta) < k) --b;
+        bprev = b;
+        atomicAdd(&h1[b], af);
+        atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
+  __syncthreads();
+  unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
+  unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
+  for (int b = threadIdx.x; b <= n; b += blockDim.x) {
+    if (h1[b]) atomicAdd(&g1[b], h1[b]);
+    if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
+  }
+  if (threadIdx.x == 0) atomicAdd(&v.s2[slot], red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void k_mse_select(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                    int ncand, int bits, int slot, int force_all) {
+  const MseView& v = mview(d, qj, blockIdx.x);
+  if (v.done && *v.done) return;
+  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) {
+    if (threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }   // finalize emits NaN for degenerate mx
+    return;
+  }
+  const int n = ncand;
+  if (force_all || n > kMaxStage1) {
+    if (threadIdx.x == 0) { sel[0] = n; sel[1] = -1; }
+    return;
+  }
+  __shared__ unsigned long long h1[kMaxStage1 + 1], h2[kMaxStage1 + 1];
+  __shared__ double lo[kMaxStage1], hi[kMaxStage1];
+  __shared__ double wmin[4];
+  const unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
+  const unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
+  for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = g1[b]; h2[b] = g2[b]; }
+  __syncthreads();
+  const int qmax = 1 << (bits - 1);
+  const double den = (double)(2 * qmax - 1);
+  int emx;
+  (void)__builtin_frexpf(mx, &emx);
+  const long long nterm = (long long)v.nelem * qmax;
+  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
+  const int K1 = 61 - emx - clt;
+  const int K = fixed_exp(mx, v.nq);
+  const double S2 = v.s2[slot];
+  const double u = 0x1p-24;
+  double mymin = 1e300;
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    unsigned long long t1 = 0ull, t2 = 0ull;
+    for (int b = c + 1; b <= n; ++b) { t1 += h1[b]; t2 += h2[b]; }
+    const double s = (double)((2.0f * cand_t(mx, c, n)) / (float)den);
+    const double T1 = (double)t1 * ldexp(1.0, -K1);
+    const double T2 = (double)t2;
+    const double A = S2 - 2.0 * s * T1 + s * s * T2;
+    const double mag = S2 + 2.0 * s * T1 + s * s * T2;
+    const double slack = 1e-10 * mag;
+    const double sh = fmax(A, 0.0) + slack;
+    const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
+    const double E = B1 + 3.0000002 * u * (sh + B1) + (double)v.nq * ldexp(1.0, -K) +
+                     2.0 * s * (double)nterm * ldexp(1.0, -K1) + slack + 8.0 * (double)v.nelem * 0x1p-149;
+    lo[c] = A - E;
+    hi[c] = A + E;
+    mymin = fmin(mymin, A + E);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mymin = fmin(mymin, __shfl_xor(mymin, off));
+  if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = mymin;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double best = fmin(fmin(wmin[0], wmin[1]), fmin(wmin[2], wmin[3]));
+    int ns = 0;
+    for (int c = 0; c < n; ++c) {
+      if (lo[c] <= best) {
+        if (ns < kMaxSel) sel[2 + ns] = c;
+        ++ns;
+      }
+    }
+    if (ns > kMaxSel || ns == 0) { sel[0] = n; sel[1] = -1; }    // exhaustive fallback
+    else { sel[0] = ns; sel[1] = sel[2]; }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                 const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
+  const Chunk ck = chunks[blockIdx.x];
+  const MseView& v = mview(d, qj, ck.job);
+  if (v.done && *v.done) return;
+  const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  const int ns = sel[0];
+  if (ns == 1) return;
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) return;
+  __shared__ float4 xs[kSseQuads];
+  __shared__ int list[kMaxSel];
+  const int nqc = min(kSseQuads, v.nq - ck.start);
+  for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
+    const int qi = ck.start + t;
+    const int row = qi / v.qpr;
+    const int qc = qi - row * v.qpr;
+    xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+  }
+  const bool all = ns >= ncand;
+  if (!all)
+    for (int j = threadIdx.x; j < ns; j += blockDim.x) list[j] = sel[2 + j];
+  __syncthreads();
+  sse_sweep_list(xs, nqc, mx, fixed_exp(mx, v.nq), ncand, bits, all ? nullptr : list, all ? ncand : ns,
+                 v.sse + (size_t)slot * ncand);
+}
+
+void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                     int slot, hipStream_t s) {
+  if (nchunks > 0) hipLaunchKernelGGL(k_mse_hist, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+}
+void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
+                       hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(k_mse_select, dim3(njobs), dim3(256), 0, s, d, q, ncand, bits, slot, force_all);
+}
+void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                    int slot, hipStream_t s) {
+  if (nchunks > 0) hipLaunchKernelGGL(k_mse_sse, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+}
+
+}  // namespace admmq

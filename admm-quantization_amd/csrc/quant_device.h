@@ -158,65 +158,76 @@ __device__ __forceinline__ int wave_argmin_u64(const unsigned long long* sse, in
 }
 
 // ---------------------------------------------------------------------------
-// The 200-candidate SSE sweep over one chunk of quads held in LDS.
-// Lane -> candidate mapping per 64-candidate group g: cnt = min(64, n-64g)
-// candidates over p2 = pow2ceil(cnt) lanes, S = 64/p2 interleaved quad streams.
-// Each lane accumulates its canonical fixed-point SSE and the group's S streams
-// are folded with xor-shuffles; lanes of stream 0 add into sse[] atomically.
+// Canonical SSE of a candidate list over one chunk of quads held in LDS (stage 2 of
+// the search, or the exhaustive sweep when list == nullptr: candidates 0..nc-1).
+// Lane -> candidate mapping per 64-candidate group g: cnt = min(64, nc-64g)
+// candidates over p2 = pow2ceil(cnt) lanes and S = 64/p2 interleaved quad streams;
+// when there are fewer groups than waves, the waves of a group split the quads too.
+// Each lane accumulates the canonical fixed-point SSE; streams fold with xor-shuffles
+// and stream 0 adds into sse[candidate] atomically (integer adds: order-free).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void sse_sweep(const float4* __restrict__ xs, int nqc, float mx, int K, int ncand,
-                                          int bits, unsigned long long* __restrict__ sse) {
+__device__ __forceinline__ void sse_group(const float4* __restrict__ xs, int nqc, float mx, int K, int ncand,
+                                          int bits, const int* list, int nc, int g, int wsub, int wpg,
+                                          unsigned long long* __restrict__ sse) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwaves = blockDim.x >> 6;
   const int q = 1 << (bits - 1);
   const float qlo = (float)(-q), qhi = (float)(q - 1);
   const float den = (float)(2 * q - 1);
   // near-half-integer window for the reciprocal fast path: > 3 ulp of |y| <= q+1
   const float delta = (float)(q + 1) * 0x1p-21f;
-  const int ngroups = (ncand + 63) >> 6;
-  for (int g = wave; g < ngroups; g += nwaves) {
-    const int cnt = min(64, ncand - 64 * g);
-    int lg = 0;
-    while ((1 << lg) < cnt) ++lg;
-    const int p2 = 1 << lg;
-    const int S = 64 >> lg;
-    const int csub = lane & (p2 - 1);
-    const int stream = lane >> lg;
-    const bool active = csub < cnt;
-    const int c = 64 * g + (active ? csub : 0);
-    const float t = cand_t(mx, c, ncand);
-    const float s = (2.0f * t) / den;
-    const float rcp = 1.0f / s;
-    unsigned long long acc = 0;
-    for (int k = stream; k < nqc; k += S) {
-      const float4 v = xs[k];
-      float y0 = v.x * rcp, y1 = v.y * rcp, y2 = v.z * rcp, y3 = v.w * rcp;
-      float q0 = __builtin_rintf(y0), q1 = __builtin_rintf(y1), q2 = __builtin_rintf(y2), q3 = __builtin_rintf(y3);
-      // distance of each y to the nearest half-integer; one compare per quad
-      const float e0 = __builtin_fabsf(__builtin_fabsf(y0 - q0) - 0.5f);
-      const float e1 = __builtin_fabsf(__builtin_fabsf(y1 - q1) - 0.5f);
-      const float e2 = __builtin_fabsf(__builtin_fabsf(y2 - q2) - 0.5f);
-      const float e3 = __builtin_fabsf(__builtin_fabsf(y3 - q3) - 0.5f);
-      const bool nb = __builtin_fminf(__builtin_fminf(e0, e1), __builtin_fminf(e2, e3)) < delta;
-      if (__builtin_expect(nb, 0)) {   // rare: decide the rounding with the exact IEEE quotient
-        q0 = __builtin_rintf(v.x / s); q1 = __builtin_rintf(v.y / s);
-        q2 = __builtin_rintf(v.z / s); q3 = __builtin_rintf(v.w / s);
-      }
-      q0 = __builtin_amdgcn_fmed3f(q0, qlo, qhi);
-      q1 = __builtin_amdgcn_fmed3f(q1, qlo, qhi);
-      q2 = __builtin_amdgcn_fmed3f(q2, qlo, qhi);
-      q3 = __builtin_amdgcn_fmed3f(q3, qlo, qhi);
-      const float d0 = v.x - q0 * s, d1 = v.y - q1 * s, d2 = v.z - q2 * s, d3 = v.w - q3 * s;
-      const float gq = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-      acc += to_fixed(gq, K);
+  const int cnt = min(64, nc - 64 * g);
+  int lg = 0;
+  while ((1 << lg) < cnt) ++lg;
+  const int p2 = 1 << lg;
+  const int S = 64 >> lg;
+  const int csub = lane & (p2 - 1);
+  const int stream = lane >> lg;
+  const bool active = csub < cnt;
+  const int j = 64 * g + (active ? csub : 0);
+  const int c = list ? list[j] : j;
+  const float t = cand_t(mx, c, ncand);
+  const float s = (2.0f * t) / den;
+  const float rcp = 1.0f / s;
+  unsigned long long acc = 0;
+  for (int k = wsub * S + stream; k < nqc; k += wpg * S) {
+    const float4 v = xs[k];
+    const float y0 = v.x * rcp, y1 = v.y * rcp, y2 = v.z * rcp, y3 = v.w * rcp;
+    float q0 = __builtin_rintf(y0), q1 = __builtin_rintf(y1), q2 = __builtin_rintf(y2), q3 = __builtin_rintf(y3);
+    // distance of each y to the nearest half-integer; one compare per quad
+    const float e0 = __builtin_fabsf(__builtin_fabsf(y0 - q0) - 0.5f);
+    const float e1 = __builtin_fabsf(__builtin_fabsf(y1 - q1) - 0.5f);
+    const float e2 = __builtin_fabsf(__builtin_fabsf(y2 - q2) - 0.5f);
+    const float e3 = __builtin_fabsf(__builtin_fabsf(y3 - q3) - 0.5f);
+    const bool nb = __builtin_fminf(__builtin_fminf(e0, e1), __builtin_fminf(e2, e3)) < delta;
+    if (__builtin_expect(nb, 0)) {   // rare: decide the rounding with the exact IEEE quotient
+      q0 = __builtin_rintf(v.x / s); q1 = __builtin_rintf(v.y / s);
+      q2 = __builtin_rintf(v.z / s); q3 = __builtin_rintf(v.w / s);
     }
-    for (int off = p2; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
-    if (active && stream == 0) atomicAdd(&sse[64 * g + csub], acc);
+    q0 = __builtin_amdgcn_fmed3f(q0, qlo, qhi);
+    q1 = __builtin_amdgcn_fmed3f(q1, qlo, qhi);
+    q2 = __builtin_amdgcn_fmed3f(q2, qlo, qhi);
+    q3 = __builtin_amdgcn_fmed3f(q3, qlo, qhi);
+    const float d0 = v.x - q0 * s, d1 = v.y - q1 * s, d2 = v.z - q2 * s, d3 = v.w - q3 * s;
+    const float gq = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    acc += to_fixed(gq, K);
+  }
+  for (int off = p2; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
+  if (active && stream == 0) atomicAdd(&sse[c], acc);
+}
+
+__device__ __forceinline__ void sse_sweep_list(const float4* __restrict__ xs, int nqc, float mx, int K, int ncand,
+                                               int bits, const int* list, int nc, unsigned long long* __restrict__ sse) {
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const int ngroups = (nc + 63) >> 6;
+  if (ngroups >= nwaves) {
+    for (int g = wave; g < ngroups; g += nwaves) sse_group(xs, nqc, mx, K, ncand, bits, list, nc, g, 0, 1, sse);
+  } else {
+    const int wpg = nwaves / ngroups;
+    if (wave < wpg * ngroups) sse_group(xs, nqc, mx, K, ncand, bits, list, nc, wave % ngroups, wave / ngroups, wpg, sse);
   }
 }
 
-// Block-level reductions -----------------------------------------------------
 __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, off));
@@ -228,18 +239,44 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
   return v;
 }
 
-// Resolve the quantization parameters of a job/problem inside a block.
-__device__ __forceinline__ QParams block_qparams(int scheme, int bits, const unsigned* stat,
-                                                 const unsigned long long* sse, int ncand, int has_kw,
-                                                 float kw_min, float kw_max) {
+// Resolve the quantization parameters of a job inside a block (all threads call).
+// MSE: the select record gives c* directly (|S| = 1), or the canonical SSE of the
+// list / of every candidate decides (first index on ties, like torch.argmin).
+__device__ __forceinline__ QParams block_qparams(int scheme, int bits, const MseView& v, int slot, int ncand,
+                                                 int has_kw, float kw_min, float kw_max) {
   __shared__ int s_idx;
+  const unsigned* stat = v.stat + 4 * slot;
   const unsigned ab = stat[0];
   const bool has_nan = ab > 0x7F800000u;
   if (scheme == kMse) {
     const float mx = __uint_as_float(ab);
     if (mse_degenerate(mx)) return qparams_mse(bits, __builtin_nanf(""));
+    const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+    const unsigned long long* sse = v.sse + (size_t)slot * ncand;
     if (threadIdx.x < 64) {
-      const int idx = wave_argmin_u64(sse, ncand);
+      const int ns = sel[0];
+      int idx;
+      if (ns == 1) {
+        idx = sel[1];
+      } else if (ns >= ncand) {
+        idx = wave_argmin_u64(sse, ncand);
+      } else {
+        const int lane = threadIdx.x & 63;
+        unsigned long long best = ~0ull;
+        int bi = 0x7fffffff;
+        for (int j = lane; j < ns; j += 64) {
+          const int c = sel[2 + j];
+          const unsigned long long x = sse[c];
+          if (x < best || (x == best && c < bi)) { best = x; bi = c; }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const unsigned long long ov = __shfl_xor(best, off);
+          const int oi = __shfl_xor(bi, off);
+          if (ov < best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+        }
+        idx = bi;
+      }
       if (threadIdx.x == 0) s_idx = idx;
     }
     __syncthreads();

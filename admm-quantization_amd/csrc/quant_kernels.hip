@@ -1,36 +1,9 @@
-// Quantizer kernels: the MSE-minmax candidate search (source/quantization.py:118-144)
-// and the tensor_* schemes (:48-66, :91-106), for standalone quantize_tensor calls
-// and for the ADMM projection step.
+// Standalone quantize_tensor kernels (source/quantization.py:69-115): pack + tensor
+// statistics, and the final elementwise quantization with the resolved parameters.
+// The MSE-minmax candidate search itself lives in mse_search.hip.
 #include "quant_device.h"
 
 namespace admmq {
-
-// Load a chunk of quads into LDS and run the candidate sweep.
-__device__ __forceinline__ void sse_chunk(const float* __restrict__ X, int ld, int qpr, int nq, int q0,
-                                          const unsigned* stat, unsigned long long* sse, int ncand, int bits) {
-  __shared__ float4 xs[kSseQuads];
-  const float mx = __uint_as_float(stat[0]);
-  if (mse_degenerate(mx)) return;
-  const int nqc = min(kSseQuads, nq - q0);
-  for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
-    const int qi = q0 + t;
-    const int row = qi / qpr;
-    const int qc = qi - row * qpr;
-    xs[t] = *reinterpret_cast<const float4*>(X + (size_t)row * ld + 4 * qc);
-  }
-  __syncthreads();
-  sse_sweep(xs, nqc, mx, fixed_exp(mx, nq), ncand, bits, sse);
-}
-
-// ADMM projection: SSE pass over X = H_T - U of every active problem.
-__global__ __launch_bounds__(256) void k_sse_admm(const ProbDesc* __restrict__ probs, const Chunk* __restrict__ chunks,
-                                                  int ncand, int bits, int slot) {
-  const Chunk ck = chunks[blockIdx.x];
-  const ProbDesc& p = probs[ck.job];
-  if (p.flags[0]) return;
-  const int qpr = (p.R + 3) >> 2;
-  sse_chunk(p.X, p.ld, qpr, p.nq, ck.start, p.stat + 4 * slot, p.sse + (size_t)slot * ncand, ncand, bits);
-}
 
 // Standalone: pack rows x cols -> rows x ld (zero pads) and gather min/max/absmax.
 __global__ __launch_bounds__(256) void k_qpack(const QJob* __restrict__ jobs, const Chunk* __restrict__ chunks) {
@@ -66,24 +39,17 @@ __global__ __launch_bounds__(256) void k_qpack(const QJob* __restrict__ jobs, co
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       amax = max(amax, red[0][k]); mn = min(mn, red[1][k]); mxo = max(mxo, red[2][k]);
     }
-    atomicMax(&j.stat[0], amax);
-    atomicMin(&j.stat[1], mn);
-    atomicMax(&j.stat[2], mxo);
+    atomicMax(&j.mv.stat[0], amax);
+    atomicMin(&j.mv.stat[1], mn);
+    atomicMax(&j.mv.stat[2], mxo);
   }
-}
-
-__global__ __launch_bounds__(256) void k_sse_q(const QJob* __restrict__ jobs, const Chunk* __restrict__ chunks,
-                                               int ncand, int bits) {
-  const Chunk ck = chunks[blockIdx.x];
-  const QJob& j = jobs[ck.job];
-  sse_chunk(j.Xp, j.ld, j.ld >> 2, j.nq, ck.start, j.stat, j.sse, ncand, bits);
 }
 
 __global__ __launch_bounds__(256) void k_qfinal(const QJob* __restrict__ jobs, const Chunk* __restrict__ chunks,
                                                 int ncand, int bits, int scheme) {
   const Chunk ck = chunks[blockIdx.x];
   const QJob& j = jobs[ck.job];
-  const QParams qp = block_qparams(scheme, bits, j.stat, j.sse, ncand, j.has_kw, j.tmin_kw, j.tmax_kw);
+  const QParams qp = block_qparams(scheme, bits, j.mv, 0, ncand, j.has_kw, j.tmin_kw, j.tmax_kw);
   const long long total = (long long)j.rows * j.ld;
   const long long e = (long long)ck.start + 4LL * threadIdx.x;
   if (e >= total) return;
@@ -98,15 +64,8 @@ __global__ __launch_bounds__(256) void k_qfinal(const QJob* __restrict__ jobs, c
   }
 }
 
-void launch_sse_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
-                     hipStream_t s) {
-  if (nchunks > 0) hipLaunchKernelGGL(k_sse_admm, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, slot);
-}
 void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s) {
   if (nchunks > 0) hipLaunchKernelGGL(k_qpack, dim3(nchunks), dim3(256), 0, s, jobs, chunks);
-}
-void launch_sse_q(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, hipStream_t s) {
-  if (nchunks > 0) hipLaunchKernelGGL(k_sse_q, dim3(nchunks), dim3(256), 0, s, jobs, chunks, ncand, bits);
 }
 void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
                    hipStream_t s) {

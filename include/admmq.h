@@ -93,6 +93,12 @@ int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, 
 int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,
                             uint64_t* sse_out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* A/B switch for the MSE-minmax search: 1 = evaluate the canonical SSE of every
+ * candidate (the reference's 200 full passes), 0 (default) = two-stage exact search
+ * (level-breakpoint bounds, then the canonical SSE only for candidates that can still
+ * be the argmin). Both return bit-identical results. */
+int32_t admmq_set_exhaustive_search(int32_t enable);
+
 /* Optional HIP-event timing of every launch class issued by admmq_admm_prepare/run on
  * this thread between begin and end: class 0 GEMM (solve), 1 MSE candidate sweep,
  * 2 projection/dual update, 3 whole prepare phase. end() synchronises on the last event

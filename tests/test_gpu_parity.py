@@ -81,6 +81,47 @@ def test_sse_table_matches_oracle(torch_dev, shape, bits, na):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_two_stage_search_equals_exhaustive(torch_dev, seed):
+    """The default two-stage search returns exactly the exhaustive sweep's answer."""
+    torch, dev = torch_dev
+    from admmq import quantize_batched
+    from admmq._lib import exhaustive_search
+    rng = np.random.default_rng(100 + seed)
+    shapes = [(9, 134), (512, 1141), (64, 278), (3, 5), (128, 759), (1, 1)]
+    xs = []
+    for sh in shapes:
+        x = rng.standard_normal(sh) * 10.0 ** rng.uniform(-4, 1)
+        if seed % 2:
+            x.flat[rng.integers(x.size)] *= 30.0
+        xs.append(_t(torch, dev, x.astype(np.float32)))
+    for bits in (2, 4, 8):
+        fast = quantize_batched(xs, bits, MSE)
+        with exhaustive_search():
+            slow = quantize_batched(xs, bits, MSE)
+        for f, s_ in zip(fast, slow):
+            assert _bits_equal(f.cpu().numpy(), s_.cpu().numpy())
+
+
+def test_two_stage_admm_equals_exhaustive(torch_dev):
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    from admmq._lib import exhaustive_search
+    probs_np = [_layer_problem(l, m) for l, m in [("layer1.0.conv1", 0), ("layer3.1.conv2", 1), ("layer4.1.conv1", 2)]]
+
+    def run():
+        ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+              for H, F, G in probs_np]
+        Hs = admm_iteration_batched(ps, 8, 0.0, 4, MSE)
+        return [(h.cpu().numpy(), p[1].cpu().numpy()) for h, p in zip(Hs, ps)]
+
+    fast = run()
+    with exhaustive_search():
+        slow = run()
+    for f, s_ in zip(fast, slow):
+        assert _bits_equal(f[0], s_[0]) and _bits_equal(f[1], s_[1])
+
+
 def test_quantize_batched_equals_single(torch_dev):
     torch, dev = torch_dev
     from admmq import quantize_batched, quantize_tensor

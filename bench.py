@@ -169,6 +169,8 @@ def main():
     ap.add_argument("--shard", choices=["replica", "layers"], default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
+    ap.add_argument("--exhaustive", action="store_true",
+                    help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,6 +183,7 @@ def main():
 
     from admmq import _lib
     lib = _lib.load()
+    lib.admmq_set_exhaustive_search(1 if a.exhaustive else 0)
     work = build_workload(a.model, rank, world, a.shard, device)
     fi_per_step = sum(len(s.shape) * (a.max_iter_admm - 1) for (s, _, _, _) in work)
 
@@ -228,7 +231,8 @@ def main():
                                       f"{a.max_iter_admm - 1} ADMM iters (eps=0), 4-bit mse-minmax, rate 2.0",
                           "factor_iterations_per_step_per_gpu": fi_per_step, "max_iter_admm": a.max_iter_admm,
                           "parallelism": f"{'replica' if a.shard == 'replica' else 'layer-shard'} x{world}, "
-                                         "one RCCL gather of factors per step"}}
+                                         "one RCCL gather of factors per step",
+                          "mse_search": "exhaustive" if a.exhaustive else "two-stage exact"}}
         if kern is not None:
             sse_f, gemm_f = algorithmic_flops(work, a.max_iter_admm)
             sse_f *= a.steps
@@ -242,7 +246,7 @@ def main():
             rf_gemm["frac"] = rf_gemm["achieved"] / PEAK_F32
             dom = max(range(3), key=lambda k: ms[k])
             out["roofline"] = rf_sse if dom == 1 else rf_gemm
-            out["roofline"]["kernel"] = ["k_gemm (solve, MFMA f32)", "k_sse_admm (200-candidate sweep)",
+            out["roofline"]["kernel"] = ["k_gemm (solve, MFMA f32)", "MSE search (k_mse_hist/select/sse)",
                                          "k_finalize_admm"][dom]
             out["roofline_gemm"] = rf_gemm
             out["kernel_ms_per_step"] = {"gemm": ms[0] / a.steps, "sse": ms[1] / a.steps,

@@ -64,6 +64,10 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
   const long long total = (long long)v.rows * v.ld;
   const long long end = min((long long)ck.start + kHistElems, total);
   double s2 = 0.0;
+  // b = n ("level >= k for every candidate") is by far the most common breakpoint for
+  // small k: accumulate it in registers instead of 64-way-colliding LDS atomics.
+  unsigned long long full1 = 0ull;
+  unsigned full2 = 0u;
   for (long long e = (long long)ck.start + 4LL * threadIdx.x; e < end; e += 4LL * blockDim.x) {
     const float4 x4 = *reinterpret_cast<const float4*>(v.X + e);
     const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
@@ -77,14 +81,20 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
       const int k0 = min(level_of(a, 0, s_tab, r_tab, delta), cap);
       if (k0 <= 0) continue;
       const unsigned long long af = to_fixed(a, K1);
+      // levels reached even at the largest candidate count for every c
+      const int kfull = min(level_of(a, n - 1, s_tab, r_tab, delta), k0);
+      if (kfull > 0) {
+        full1 += af * (unsigned long long)kfull;
+        full2 += (unsigned)(kfull * kfull);        // sum_{k<=kfull} (2k-1)
+      }
       int bprev = n;
-      for (int k = 1; k <= k0; ++k) {
+      for (int k = kfull + 1; k <= k0; ++k) {
         // |q(c)| >= k  <=>  t_c <~ a*den/(2k-1);  t_c ~ S0 + c*step
         const float tau = a * den * __builtin_amdgcn_rcpf((float)(2 * k - 1));   // estimate only
         const float ce = (tau - S0) * inv_step;
-        int b = (ce >= (float)n) ? n : (ce < 0.f ? 1 : (int)ce + 1);
-        b = min(max(b, 1), bprev);
-        while (b < n && level_of(a, b, s_tab, r_tab, delta) >= k) ++b;
+        int b = (ce >= (float)n) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
+        b = min(max(b, 1), min(bprev, n - 1));
+        while (b < n - 1 && level_of(a, b, s_tab, r_tab, delta) >= k) ++b;
         while (b > 1 && level_of(a, b - 1, s_tab, r_tab, delta) < k) --b;
         bprev = b;
         atomicAdd(&h1[b], af);
@@ -93,8 +103,16 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
     }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
+  for (int off = 32; off > 0; off >>= 1) {
+    s2 += __shfl_xor(s2, off);
+    full1 += __shfl_xor(full1, off);
+    full2 += (unsigned)__shfl_xor((int)full2, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = s2;
+    atomicAdd(&h1[n], full1);
+    atomicAdd(&h2[n], full2);
+  }
   __syncthreads();
   unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
   unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
@@ -105,30 +123,52 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
   if (threadIdx.x == 0) atomicAdd(&v.s2[slot], red[0] + red[1] + red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void k_mse_select(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                    int ncand, int bits, int slot, int force_all) {
+// One wave per job. Lane l owns the consecutive candidate block [l*P, l*P+P) with
+// P = ceil(n/64): suffix sums come from a per-lane pass plus a wave-level exclusive
+// suffix scan, the set S is built in ascending order from a prefix count over lanes.
+__global__ __launch_bounds__(64) void k_mse_select(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                   int ncand, int bits, int slot, int force_all) {
   const MseView& v = mview(d, qj, blockIdx.x);
   if (v.done && *v.done) return;
   int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  const int lane = threadIdx.x;
   const float mx = __uint_as_float(v.stat[4 * slot]);
   if (mse_degenerate(mx)) {
-    if (threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }   // finalize emits NaN for degenerate mx
+    if (lane == 0) { sel[0] = 1; sel[1] = 0; }   // finalize emits NaN for degenerate mx
     return;
   }
   const int n = ncand;
   if (force_all || n > kMaxStage1) {
-    if (threadIdx.x == 0) { sel[0] = n; sel[1] = -1; }
+    if (lane == 0) { sel[0] = n; sel[1] = -1; }
     return;
   }
-  __shared__ unsigned long long h1[kMaxStage1 + 1], h2[kMaxStage1 + 1];
-  __shared__ double lo[kMaxStage1], hi[kMaxStage1];
-  __shared__ double wmin[4];
+  constexpr int PMAX = (kMaxStage1 + 63) / 64;
+  const int P = (n + 63) / 64;
   const unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
   const unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
-  for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = g1[b]; h2[b] = g2[b]; }
-  __syncthreads();
+  // T(c) = sum_{b > c} h[b]: lane-local suffix over its block, then across lanes
+  unsigned long long t1[PMAX], t2[PMAX];
+  unsigned long long r1 = 0ull, r2 = 0ull;
+#pragma unroll
+  for (int j = PMAX - 1; j >= 0; --j) {
+    t1[j] = r1; t2[j] = r2;                       // exclusive within the lane: b > c
+    const int b = lane * P + j;
+    if (j < P && b <= n) { r1 += g1[b]; r2 += g2[b]; }
+  }
+  // candidates above this lane's block contribute sum of later lanes' blocks, plus b = n
+  // when it is not inside any block (n == 64 P exactly).
+  unsigned long long s1 = r1, s2v = r2;          // inclusive suffix scan over lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o1 = __shfl_down(s1, off);
+    const unsigned long long o2 = __shfl_down(s2v, off);
+    if (lane + off < 64) { s1 += o1; s2v += o2; }
+  }
+  unsigned long long above1 = __shfl_down(s1, 1), above2 = __shfl_down(s2v, 1);
+  if (lane == 63) { above1 = 0ull; above2 = 0ull; }
+  if (64 * P == n) { above1 += g1[n]; above2 += g2[n]; }   // b = n lies past every block
   const int qmax = 1 << (bits - 1);
-  const double den = (double)(2 * qmax - 1);
+  const float denf = (float)(2 * qmax - 1);
   int emx;
   (void)__builtin_frexpf(mx, &emx);
   const long long nterm = (long long)v.nelem * qmax;
@@ -137,39 +177,52 @@ __global__ __launch_bounds__(256) void k_mse_select(const ProbDesc* __restrict__
   const int K = fixed_exp(mx, v.nq);
   const double S2 = v.s2[slot];
   const double u = 0x1p-24;
+  const double fixu = ldexp(1.0, -K1);
+  double lo[PMAX], hi[PMAX];
   double mymin = 1e300;
-  for (int c = threadIdx.x; c < n; c += blockDim.x) {
-    unsigned long long t1 = 0ull, t2 = 0ull;
-    for (int b = c + 1; b <= n; ++b) { t1 += h1[b]; t2 += h2[b]; }
-    const double s = (double)((2.0f * cand_t(mx, c, n)) / (float)den);
-    const double T1 = (double)t1 * ldexp(1.0, -K1);
-    const double T2 = (double)t2;
-    const double A = S2 - 2.0 * s * T1 + s * s * T2;
-    const double mag = S2 + 2.0 * s * T1 + s * s * T2;
-    const double slack = 1e-10 * mag;
-    const double sh = fmax(A, 0.0) + slack;
-    const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
-    const double E = B1 + 3.0000002 * u * (sh + B1) + (double)v.nq * ldexp(1.0, -K) +
-                     2.0 * s * (double)nterm * ldexp(1.0, -K1) + slack + 8.0 * (double)v.nelem * 0x1p-149;
-    lo[c] = A - E;
-    hi[c] = A + E;
-    mymin = fmin(mymin, A + E);
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) {
+    const int c = lane * P + j;
+    lo[j] = 1e300; hi[j] = 1e300;
+    if (j < P && c < n) {
+      const double s = (double)((2.0f * cand_t(mx, c, n)) / denf);
+      const double T1 = (double)(t1[j] + above1) * fixu;
+      const double T2 = (double)(t2[j] + above2);
+      const double A = S2 - 2.0 * s * T1 + s * s * T2;
+      const double mag = S2 + 2.0 * s * T1 + s * s * T2;
+      const double slack = 1e-10 * mag;
+      const double sh = fmax(A, 0.0) + slack;
+      const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
+      const double E = B1 + 3.0000002 * u * (sh + B1) + (double)v.nq * ldexp(1.0, -K) +
+                       2.0 * s * (double)nterm * fixu + slack + 8.0 * (double)v.nelem * 0x1p-149;
+      lo[j] = A - E;
+      hi[j] = A + E;
+      mymin = fmin(mymin, hi[j]);
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) mymin = fmin(mymin, __shfl_xor(mymin, off));
-  if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = mymin;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double best = fmin(fmin(wmin[0], wmin[1]), fmin(wmin[2], wmin[3]));
-    int ns = 0;
-    for (int c = 0; c < n; ++c) {
-      if (lo[c] <= best) {
-        if (ns < kMaxSel) sel[2 + ns] = c;
-        ++ns;
-      }
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) cnt += (lo[j] <= mymin) ? 1 : 0;
+  int pre = cnt;                                   // inclusive prefix over lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(pre, off);
+    if (lane >= off) pre += o;
+  }
+  const int total = __shfl(pre, 63);
+  int pos = pre - cnt;
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) {
+    if (lo[j] <= mymin) {
+      if (pos < kMaxSel) sel[2 + pos] = lane * P + j;
+      ++pos;
     }
-    if (ns > kMaxSel || ns == 0) { sel[0] = n; sel[1] = -1; }    // exhaustive fallback
-    else { sel[0] = ns; sel[1] = sel[2]; }
+  }
+  if (lane == 0) {   // sel = {|S| (n: exhaustive), unused, S ascending...}; |S| == 1 -> c* = sel[2]
+    if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
+    else { sel[0] = total; sel[1] = 0; }
   }
 }
 
@@ -206,7 +259,7 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
 }
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(k_mse_select, dim3(njobs), dim3(256), 0, s, d, q, ncand, bits, slot, force_all);
+  if (njobs > 0) hipLaunchKernelGGL(k_mse_select, dim3(njobs), dim3(64), 0, s, d, q, ncand, bits, slot, force_all);
 }
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s) {

@@ -257,7 +257,7 @@ __device__ __forceinline__ QParams block_qparams(int scheme, int bits, const Mse
       const int ns = sel[0];
       int idx;
       if (ns == 1) {
-        idx = sel[1];
+        idx = sel[2];
       } else if (ns >= ncand) {
         idx = wave_argmin_u64(sse, ncand);
       } else {

@@ -1,8 +1,8 @@
 // Internal device/host structures of libadmmq (not part of the C-ABI).
 //
 // Memory layout in HBM (per ADMM problem = one (layer, mode) factor):
-//   Fp, H, U, P, X, HT : float32 [Ip x ld] row-major, ld = roundup(R,16),
-//                        Ip = roundup(I,32); every pad element is kept at exactly 0
+//   Fp, H, U, P, X, HT : float32 [Ip x ld] row-major, ld = roundup(R,32),
+//                        Ip = 32 if I <= 32 else roundup(I,64); pads kept at exactly 0
 //   M                  : float32 [ldm x ldm], ldm = roundup(R,64); (G+rho I)^-1,
 //                        symmetric, zero outside the R x R block
 //   A64, L64           : float64 [ldm x ldm] SPD factor / inverse-factor scratch
@@ -91,8 +91,8 @@ void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
 void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps,
-                 int ncand, hipStream_t s);
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, int slot, int iter,
+                 float eps, int ncand, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s);
@@ -109,7 +109,7 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
                    hipStream_t s);
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
-constexpr int kHistElems = 4096;    // elements per stage-1 work unit
+constexpr int kHistElems = 1024;    // elements per stage-1 work unit (one float4 per thread)
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 
 }  // namespace admmq

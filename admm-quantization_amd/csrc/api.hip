@@ -96,6 +96,7 @@ struct AdmmPlan {
   Chunk* d_hist = nullptr;
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
+  int ntiles_big = 0, ntiles_small = 0;
 };
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
@@ -112,8 +113,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.F_user = a.F; d.G_user = a.G; d.H0_user = a.H0; d.H_out = a.H_out; d.U_user = a.U;
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
-    d.ld = rup(a.R, 16);
-    d.Ip = rup(a.I, 32);
+    d.ld = rup(a.R, 32);
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, 64);
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -135,15 +136,22 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
   }
   // GEMM tiles, longest K first (LPT over the grid); `first` marks tile (0,0).
+  // 64x64 tiles (Ip > 32) first, then the 32x64 tiles of the thin (I <= 32) factors.
   pl.tiles.clear();
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  std::vector<GemmTile> small;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
-    for (int tm = 0; tm < d.Ip / 32; ++tm)
-      for (int tn = 0; tn < (d.ld + 63) / 64; ++tn) pl.tiles.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
+    const int bm = d.Ip == 32 ? 32 : 64;
+    std::vector<GemmTile>& dst = d.Ip == 32 ? small : pl.tiles;
+    for (int tm = 0; tm < d.Ip / bm; ++tm)
+      for (int tn = 0; tn < (d.ld + 63) / 64; ++tn) dst.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
   }
+  pl.ntiles_big = (int)pl.tiles.size();
+  pl.ntiles_small = (int)small.size();
+  pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
   pl.hist_chunks.clear();
@@ -353,13 +361,13 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   hipStream_t s = static_cast<hipStream_t>(stream);
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
-  const int ntiles = (int)pl.tiles.size(), nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
+  const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = g_exhaustive || num_attempts > kMaxStage1;
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);
-    launch_gemm(pl.d_desc, pl.d_tiles, ntiles, slot, it, eps, num_attempts, s);
+    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, slot, it, eps, num_attempts, s);
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);

@@ -3,11 +3,14 @@
 // active (layer, mode) problem. P is produced by the previous iteration's
 // finalize kernel; M is symmetric, so the B operand is read as rows of M.
 //
-// Tile 32 x 64 per 128-thread workgroup; wave w owns the 32 x 32 sub-tile at
-// columns 32w with one v_mfma_f32_32x32x2_f32 accumulator chain (16 AGPRs).
-// K-step 16 = 8 MFMAs per wave, double-buffered through LDS. The LDS images keep
-// k permuted as [row][h][m] (k = 2m + h) so every lane's 8 operands for a K-step
-// are 32 contiguous bytes (2 x ds_read_b128); rows padded to 80 B.
+// Tile (32*WM) x 64 per workgroup of 2*WM waves; wave (wm, wn) owns the 32 x 32
+// sub-tile at (32 wm, 32 wn) with one v_mfma_f32_32x32x2_f32 accumulator chain
+// (16 accumulator registers). WM = 2 (64 x 64 tiles, 256 threads) for factors with
+// I > 32, WM = 1 (32 x 64, 128 threads) for the 9-row mode-C factors.
+// K-step 32 = 16 MFMAs per wave between barriers, double-buffered through LDS with
+// register prefetch of the next K-step. The LDS images keep k permuted as
+// [row][h][m] (k = 2m + h) so a lane's 16 operands for a K-step are 64 contiguous
+// bytes (4 x ds_read_b128); rows padded to 144 B (conflict-free b128 reads).
 //
 // Epilogue: store HT, X = HT - U, and fold max|X|, min X, max X of the valid
 // region into the problem's per-iteration stat slot (one atomic each per block).
@@ -17,7 +20,7 @@ namespace admmq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 32, BN = 64, BK = 16, LROW = 20;  // LDS row = 16 floats + 4 pad
+constexpr int BN = 64, BK = 32, LROW = 36;  // LDS row = 32 floats + 4 pad
 
 __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_prev, int iter, float eps) {
   if (iter == 0) return false;
@@ -27,8 +30,13 @@ __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_pre
   return (rr < (double)eps) && (ss < (double)eps);
 }
 
-__global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
-                                              int slot, int iter, float eps, int ncand) {
+template <int WM>
+__global__ __launch_bounds__(128 * WM) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
+                                                   int slot, int iter, float eps, int ncand) {
+  constexpr int BM = 32 * WM;
+  constexpr int NT = 128 * WM;                 // threads
+  constexpr int AV = BM * (BK / 4) / NT;       // float4 loads of A per thread per K-step (= 2)
+  constexpr int BV = BN * (BK / 4) / NT;       // float4 loads of B per thread per K-step (= 4 / WM)
   const GemmTile tl = tiles[blockIdx.x];
   const ProbDesc& p = probs[tl.prob];
   if (p.flags[0]) return;
@@ -40,7 +48,7 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
     unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
     unsigned long long* h1 = p.mv.h1 + (size_t)slot * (ncand + 1);
     unsigned long long* h2 = p.mv.h2 + (size_t)slot * (ncand + 1);
-    for (int c = threadIdx.x; c <= ncand; c += blockDim.x) {
+    for (int c = threadIdx.x; c <= ncand; c += NT) {
       if (c < ncand) sse[c] = 0ull;
       h1[c] = 0ull;
       h2[c] = 0ull;
@@ -54,33 +62,37 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const int wm = wave / 2, wn = wave & 1;
   const int ld = p.ld, ldm = p.ldm;
   const int row0 = tl.tm * BM, col0 = tl.tn * BN;
   const float* __restrict__ P = p.P;
   const float* __restrict__ M = p.M;
 
-  // global -> register staging indices
-  const int ar = tid >> 2, aq = tid & 3;            // A: 32 rows x 4 float4
-  const float* aptr = P + (size_t)(row0 + ar) * ld + 4 * aq;
-  const float* bptr0 = M + (size_t)(col0 + ar) * ldm + 4 * aq;        // B rows ar and ar+32
-  const float* bptr1 = M + (size_t)(col0 + ar + 32) * ldm + 4 * aq;
-
-  float4 ra, rb0, rb1;
+  // staging: element v of thread t covers row (t + v*NT) / 8, k-quad (t % 8)
+  const int kq = tid & 7;
+  const int r0 = tid >> 3;
+  float4 ra[AV], rb[BV];
   auto gload = [&](int k0) {
-    ra = *reinterpret_cast<const float4*>(aptr + k0);
-    rb0 = *reinterpret_cast<const float4*>(bptr0 + k0);
-    rb1 = *reinterpret_cast<const float4*>(bptr1 + k0);
+#pragma unroll
+    for (int v = 0; v < AV; ++v)
+      ra[v] = *reinterpret_cast<const float4*>(P + (size_t)(row0 + r0 + v * (NT / 8)) * ld + k0 + 4 * kq);
+#pragma unroll
+    for (int v = 0; v < BV; ++v)
+      rb[v] = *reinterpret_cast<const float4*>(M + (size_t)(col0 + r0 + v * (NT / 8)) * ldm + k0 + 4 * kq);
   };
   auto sstore = [&](int b) {
-    float* a = &As[b][ar * LROW + 2 * aq];
-    *reinterpret_cast<float2*>(a) = make_float2(ra.x, ra.z);
-    *reinterpret_cast<float2*>(a + 8) = make_float2(ra.y, ra.w);
-    float* b0 = &Bs[b][ar * LROW + 2 * aq];
-    *reinterpret_cast<float2*>(b0) = make_float2(rb0.x, rb0.z);
-    *reinterpret_cast<float2*>(b0 + 8) = make_float2(rb0.y, rb0.w);
-    float* b1 = &Bs[b][(ar + 32) * LROW + 2 * aq];
-    *reinterpret_cast<float2*>(b1) = make_float2(rb1.x, rb1.z);
-    *reinterpret_cast<float2*>(b1 + 8) = make_float2(rb1.y, rb1.w);
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      float* a = &As[b][(r0 + v * (NT / 8)) * LROW + 2 * kq];
+      *reinterpret_cast<float2*>(a) = make_float2(ra[v].x, ra[v].z);
+      *reinterpret_cast<float2*>(a + 16) = make_float2(ra[v].y, ra[v].w);
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      float* bb = &Bs[b][(r0 + v * (NT / 8)) * LROW + 2 * kq];
+      *reinterpret_cast<float2*>(bb) = make_float2(rb[v].x, rb[v].z);
+      *reinterpret_cast<float2*>(bb + 16) = make_float2(rb[v].y, rb[v].w);
+    }
   };
 
   f32x16 acc;
@@ -95,28 +107,27 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * BK);
-    const float4* ap = reinterpret_cast<const float4*>(&As[cur][i * LROW + 8 * h]);
-    const float4* bp = reinterpret_cast<const float4*>(&Bs[cur][(32 * wave + i) * LROW + 8 * h]);
-    const float4 a0 = ap[0], a1 = ap[1], b0 = bp[0], b1 = bp[1];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b0.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b0.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b0.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b0.w, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b1.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b1.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, b1.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, b1.w, acc, 0, 0, 0);
+    const float4* ap = reinterpret_cast<const float4*>(&As[cur][(32 * wm + i) * LROW + 16 * h]);
+    const float4* bp = reinterpret_cast<const float4*>(&Bs[cur][(32 * wn + i) * LROW + 16 * h]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a = ap[q], b = bp[q];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+    }
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
 
   // epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-  const int col = col0 + 32 * wave + i;
+  const int col = col0 + 32 * wn + i;
   unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
   if (col < ld) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
       const size_t off = (size_t)row * ld + col;
       const float ht = acc[r];
       const float x = ht - p.U[off];
@@ -131,20 +142,28 @@ __global__ __launch_bounds__(128) void k_gemm(const ProbDesc* __restrict__ probs
     }
   }
   amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
-  __shared__ unsigned red[3][2];
+  __shared__ unsigned red[3][2 * WM];
   if (lane == 0) { red[0][wave] = amax; red[1][wave] = mn; red[2][wave] = mxo; }
   __syncthreads();
   if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < 2 * WM; ++w) {
+      red[0][0] = max(red[0][0], red[0][w]); red[1][0] = min(red[1][0], red[1][w]); red[2][0] = max(red[2][0], red[2][w]);
+    }
     unsigned* st = p.mv.stat + 4 * slot;
-    atomicMax(&st[0], max(red[0][0], red[0][1]));
-    atomicMin(&st[1], min(red[1][0], red[1][1]));
-    atomicMax(&st[2], max(red[2][0], red[2][1]));
+    atomicMax(&st[0], red[0][0]);
+    atomicMin(&st[1], red[1][0]);
+    atomicMax(&st[2], red[2][0]);
   }
 }
 
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
-                 hipStream_t s) {
-  if (ntiles > 0) hipLaunchKernelGGL(k_gemm, dim3(ntiles), dim3(128), 0, s, d, tiles, slot, iter, eps, ncand);
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, int slot, int iter,
+                 float eps, int ncand, hipStream_t s) {
+  // tiles[0 .. ntiles_big) are 64x64 (WM=2), then ntiles_small 32x64 tiles (WM=1)
+  if (ntiles_big > 0)
+    hipLaunchKernelGGL(k_gemm<2>, dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
+  if (ntiles_small > 0)
+    hipLaunchKernelGGL(k_gemm<1>, dim3(ntiles_small), dim3(128), 0, s, d, tiles + ntiles_big, slot, iter, eps, ncand);
 }
 
 }  // namespace admmq

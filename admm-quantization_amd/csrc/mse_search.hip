@@ -14,6 +14,8 @@
 //                       S = {c : A - E <= min(A + E)} provably holds the argmin.
 // stage 2  k_mse_sse    canonical SSE only for c in S (|S| = 1 almost always: then the
 //                       kernel exits at once); exhaustive when |S| > kMaxSel or forced.
+#include <cstdlib>
+
 #include "quant_device.h"
 
 namespace admmq {
@@ -31,6 +33,9 @@ __device__ __forceinline__ int level_of(float a, int c, const float* __restrict_
   return (int)q;
 }
 
+// VAR (timing ablation only, results wrong unless 0): 1 = no LDS histogram atomics,
+// 2 = no global flush, 3 = neither.
+template <int VAR>
 __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
                                                   const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
   const Chunk ck = chunks[blockIdx.x];
@@ -97,8 +102,12 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
         while (b < n - 1 && level_of(a, b, s_tab, r_tab, delta) >= k) ++b;
         while (b > 1 && level_of(a, b - 1, s_tab, r_tab, delta) < k) --b;
         bprev = b;
-        atomicAdd(&h1[b], af);
-        atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+        if constexpr (VAR & 1) {
+          full1 += af ^ (unsigned long long)b;
+        } else {
+          atomicAdd(&h1[b], af);
+          atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+        }
       }
     }
   }
@@ -116,9 +125,13 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
   __syncthreads();
   unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
   unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
-  for (int b = threadIdx.x; b <= n; b += blockDim.x) {
-    if (h1[b]) atomicAdd(&g1[b], h1[b]);
-    if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
+  if constexpr ((VAR & 2) == 0) {
+    for (int b = threadIdx.x; b <= n; b += blockDim.x) {
+      if (h1[b]) atomicAdd(&g1[b], h1[b]);
+      if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
+    }
+  } else {
+    if (threadIdx.x == 0 && h1[n] == 12345) g1[0] = h2[0];
   }
   if (threadIdx.x == 0) atomicAdd(&v.s2[slot], red[0] + red[1] + red[2] + red[3]);
 }
@@ -255,7 +268,15 @@ __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d,
 
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s) {
-  if (nchunks > 0) hipLaunchKernelGGL(k_mse_hist, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  static const int var = [] {
+    const char* e = getenv("ADMMQ_HIST_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  if (nchunks <= 0) return;
+  if (var == 1) hipLaunchKernelGGL(k_mse_hist<1>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  else if (var == 2) hipLaunchKernelGGL(k_mse_hist<2>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  else if (var == 3) hipLaunchKernelGGL(k_mse_hist<3>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  else hipLaunchKernelGGL(k_mse_hist<0>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
 }
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s) {

@@ -20,6 +20,8 @@ enum QScheme { kMse = 0, kMinMax = 1, kSymmetric = 2, kAffine = 3 };
 
 constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaustive)
 constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
+constexpr int kMaxStage1Bits = 6;  // bits handled by the two-stage search (threshold table in LDS)
+constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms (atomic spread)
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
@@ -33,8 +35,8 @@ struct MseView {
   int nq, nelem;               // quads of the valid region, rows*cols
   unsigned* stat;              // [slot][4] {absmax bits, min enc, max enc, 0}
   unsigned long long* sse;     // [slot][ncand] canonical fixed-point SSE
-  unsigned long long* h1;      // [slot][ncand+1]
-  unsigned long long* h2;      // [slot][ncand+1]
+  unsigned long long* h1;      // [slot][kHistRep][ncand+1]
+  unsigned long long* h2;      // [slot][kHistRep][ncand+1]
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
   const int* done;             // early-exit flag (ADMM) or nullptr
@@ -96,6 +98,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s);
+size_t hist_lds_bytes(int ncand, int bits);
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
@@ -109,7 +112,7 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
                    hipStream_t s);
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
-constexpr int kHistElems = 1024;    // elements per stage-1 work unit (one float4 per thread)
+constexpr int kHistElems = 4096;    // elements per stage-1 work unit (1024 threads x float4)
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 
 }  // namespace admmq

@@ -53,6 +53,11 @@ static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
 
+// The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
+static bool two_stage_ok(int ncand, int bits) {
+  return !g_exhaustive && ncand <= kMaxStage1 && bits <= kMaxStage1Bits && hist_lds_bytes(ncand, bits) <= 64 * 1024;
+}
+
 static inline void prof_mark(hipStream_t s) {
   if (!g_prof.on || g_prof.next >= g_prof.ev.size()) return;
   (void)hipEventRecord(g_prof.ev[g_prof.next++], s);
@@ -79,8 +84,8 @@ struct Carver {
 static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.stat = cv.take<unsigned>(4 * (size_t)nslot);
   v.sse = cv.take<unsigned long long>((size_t)nslot * ncand);
-  v.h1 = cv.take<unsigned long long>((size_t)nslot * (ncand + 1));
-  v.h2 = cv.take<unsigned long long>((size_t)nslot * (ncand + 1));
+  v.h1 = cv.take<unsigned long long>((size_t)nslot * kHistRep * (ncand + 1));
+  v.h2 = cv.take<unsigned long long>((size_t)nslot * kHistRep * (ncand + 1));
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
 }
@@ -243,11 +248,8 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
 
 __global__ void k_qinit(QJob* jobs, int n, int ncand) {
   const MseView& v = jobs[blockIdx.x].mv;
-  for (int c = threadIdx.x; c <= ncand; c += blockDim.x) {
-    if (c < ncand) v.sse[c] = 0ull;
-    v.h1[c] = 0ull;
-    v.h2[c] = 0ull;
-  }
+  for (int c = threadIdx.x; c < ncand; c += blockDim.x) v.sse[c] = 0ull;
+  for (int c = threadIdx.x; c < kHistRep * (ncand + 1); c += blockDim.x) { v.h1[c] = 0ull; v.h2[c] = 0ull; }
   if (threadIdx.x == 0) {
     v.stat[0] = 0u; v.stat[1] = 0xFFFFFFFFu; v.stat[2] = 0u; v.stat[3] = 0u;
     v.s2[0] = 0.0;
@@ -269,7 +271,7 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   hipLaunchKernelGGL(k_qinit, dim3(n), dim3(256), 0, s, pl.d_jobs, n, ncand);
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
   if (qscheme == kMse) {
-    const bool all = exhaustive || ncand > kMaxStage1;
+    const bool all = exhaustive || !two_stage_ok(ncand, bits);
     if (!all) launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
     launch_mse_select(nullptr, pl.d_jobs, n, ncand, bits, 0, all ? 1 : 0, s);
     launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
@@ -363,7 +365,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   if ((rc = upload_admm(pl, s))) return rc;
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
-  const bool exhaustive = g_exhaustive || num_attempts > kMaxStage1;
+  const bool exhaustive = !two_stage_ok(num_attempts, bits);
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);

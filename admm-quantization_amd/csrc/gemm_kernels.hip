@@ -46,13 +46,10 @@ __global__ __launch_bounds__(128 * WM) void k_gemm(const ProbDesc* __restrict__ 
   }
   if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
     unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
-    unsigned long long* h1 = p.mv.h1 + (size_t)slot * (ncand + 1);
-    unsigned long long* h2 = p.mv.h2 + (size_t)slot * (ncand + 1);
-    for (int c = threadIdx.x; c <= ncand; c += NT) {
-      if (c < ncand) sse[c] = 0ull;
-      h1[c] = 0ull;
-      h2[c] = 0ull;
-    }
+    unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
+    unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
+    for (int c = threadIdx.x; c < ncand; c += NT) sse[c] = 0ull;
+    for (int c = threadIdx.x; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
     if (threadIdx.x == 0) p.mv.s2[slot] = 0.0;
   }
 

@@ -14,8 +14,6 @@
 //                       S = {c : A - E <= min(A + E)} provably holds the argmin.
 // stage 2  k_mse_sse    canonical SSE only for c in S (|S| = 1 almost always: then the
 //                       kernel exits at once); exhaustive when |S| > kMaxSel or forced.
-#include <cstdlib>
-
 #include "quant_device.h"
 
 namespace admmq {
@@ -33,47 +31,69 @@ __device__ __forceinline__ int level_of(float a, int c, const float* __restrict_
   return (int)q;
 }
 
-// VAR (timing ablation only, results wrong unless 0): 1 = no LDS histogram atomics,
-// 2 = no global flush, 3 = neither.
-template <int VAR>
-__global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                  const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
+// Smallest float32 a >= 0 with rint(fl(a / s)) >= k (IEEE division, half-even ties):
+// fl(a/s) is monotone in a, so step from the estimate (k - 1/2) s by ulps.
+__device__ __forceinline__ bool reaches(float a, float s, int k) {
+  const float y = a / s;
+  const float h = (float)k - 0.5f;
+  return (y > h) || (y == h && (k & 1) == 0);
+}
+__device__ float level_threshold(float s, int k) {
+  float a = ((float)k - 0.5f) * s;
+  if (reaches(a, s, k)) {
+    for (int it = 0; it < 64; ++it) {
+      const float p = __uint_as_float(__float_as_uint(a) - 1u);
+      if (a == 0.f || !reaches(p, s, k)) break;
+      a = p;
+    }
+  } else {
+    for (int it = 0; it < 64 && !reaches(a, s, k); ++it) a = __uint_as_float(__float_as_uint(a) + 1u);
+  }
+  return a;
+}
+
+// Stage 1. thr[k][c] turns every breakpoint probe into one compare:
+// |q_c(x)| >= k  <=>  |x| >= thr[k][c]  (thr increasing in c and in k).
+// 1024 threads x 4 elements per block; the block's histograms are flushed into one of
+// kHistRep replicas of the job's global histograms (replica = block % kHistRep).
+__global__ __launch_bounds__(1024) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                   const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
   const Chunk ck = chunks[blockIdx.x];
   const MseView& v = mview(d, qj, ck.job);
   if (v.done && *v.done) return;
   const float mx = __uint_as_float(v.stat[4 * slot]);
   if (mse_degenerate(mx)) return;
-  __shared__ float s_tab[kMaxStage1], r_tab[kMaxStage1];
-  __shared__ unsigned long long h1[kMaxStage1 + 1];
-  __shared__ unsigned h2[kMaxStage1 + 1];
-  __shared__ double red[4];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = ncand;
   const int qmax = 1 << (bits - 1);
+  unsigned long long* h1 = reinterpret_cast<unsigned long long*>(smem);          // n+1
+  unsigned* h2 = reinterpret_cast<unsigned*>(h1 + (n + 1));                       // n+1
+  float* thr = reinterpret_cast<float*>(h2 + ((n + 1 + 3) & ~3));                 // [qmax+1][n]
+  __shared__ double red[16];
   const float den = (float)(2 * qmax - 1);
-  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+  for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
+    const int k = 1 + e / n, c = e - (k - 1) * n;
     const float s = (2.0f * cand_t(mx, c, n)) / den;
-    s_tab[c] = s;
-    r_tab[c] = 1.0f / s;
+    thr[k * n + c] = level_threshold(s, k);
   }
   for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
   __syncthreads();
   const float S0 = (float)(0.2 * (double)mx);
   const float E0 = (float)(1.2 * (double)mx);
   const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
-  const float delta = (float)(qmax + 1) * 0x1p-21f;
   int emx;
   (void)__builtin_frexpf(mx, &emx);
   const long long nterm = (long long)v.nelem * qmax;
   const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
   const int K1 = 61 - emx - clt;
   const long long total = (long long)v.rows * v.ld;
-  const long long end = min((long long)ck.start + kHistElems, total);
   double s2 = 0.0;
-  // b = n ("level >= k for every candidate") is by far the most common breakpoint for
-  // small k: accumulate it in registers instead of 64-way-colliding LDS atomics.
+  // b = n ("level >= k for every candidate") is the most common breakpoint for small
+  // k: accumulate it in registers instead of colliding LDS atomics.
   unsigned long long full1 = 0ull;
   unsigned full2 = 0u;
-  for (long long e = (long long)ck.start + 4LL * threadIdx.x; e < end; e += 4LL * blockDim.x) {
+  const long long e = (long long)ck.start + 4LL * threadIdx.x;
+  if (e < total) {
     const float4 x4 = *reinterpret_cast<const float4*>(v.X + e);
     const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
@@ -83,31 +103,30 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
       s2 += (double)x * (double)x;
       const float a = __builtin_fabsf(x);
       const int cap = (x > 0.f) ? qmax - 1 : qmax;
-      const int k0 = min(level_of(a, 0, s_tab, r_tab, delta), cap);
+      int k0 = 0, kfull = 0;
+      for (int k = 1; k <= cap; ++k) {
+        k0 += (a >= thr[k * n]) ? 1 : 0;
+        kfull += (a >= thr[k * n + n - 1]) ? 1 : 0;
+      }
       if (k0 <= 0) continue;
       const unsigned long long af = to_fixed(a, K1);
-      // levels reached even at the largest candidate count for every c
-      const int kfull = min(level_of(a, n - 1, s_tab, r_tab, delta), k0);
       if (kfull > 0) {
         full1 += af * (unsigned long long)kfull;
         full2 += (unsigned)(kfull * kfull);        // sum_{k<=kfull} (2k-1)
       }
-      int bprev = n;
+      int bprev = n - 1;
       for (int k = kfull + 1; k <= k0; ++k) {
-        // |q(c)| >= k  <=>  t_c <~ a*den/(2k-1);  t_c ~ S0 + c*step
+        // b_k = #{c : a >= thr[k][c]} in [1, n-1]; estimate from t_c ~ S0 + c*step
+        const float* tk = thr + k * n;
         const float tau = a * den * __builtin_amdgcn_rcpf((float)(2 * k - 1));   // estimate only
         const float ce = (tau - S0) * inv_step;
         int b = (ce >= (float)n) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
-        b = min(max(b, 1), min(bprev, n - 1));
-        while (b < n - 1 && level_of(a, b, s_tab, r_tab, delta) >= k) ++b;
-        while (b > 1 && level_of(a, b - 1, s_tab, r_tab, delta) < k) --b;
+        b = min(max(b, 1), bprev);
+        while (b < n - 1 && a >= tk[b]) ++b;
+        while (b > 1 && a < tk[b - 1]) --b;
         bprev = b;
-        if constexpr (VAR & 1) {
-          full1 += af ^ (unsigned long long)b;
-        } else {
-          atomicAdd(&h1[b], af);
-          atomicAdd(&h2[b], (unsigned)(2 * k - 1));
-        }
+        atomicAdd(&h1[b], af);
+        atomicAdd(&h2[b], (unsigned)(2 * k - 1));
       }
     }
   }
@@ -123,17 +142,23 @@ __global__ __launch_bounds__(256) void k_mse_hist(const ProbDesc* __restrict__ d
     atomicAdd(&h2[n], full2);
   }
   __syncthreads();
-  unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
-  unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
-  if constexpr ((VAR & 2) == 0) {
-    for (int b = threadIdx.x; b <= n; b += blockDim.x) {
-      if (h1[b]) atomicAdd(&g1[b], h1[b]);
-      if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
-    }
-  } else {
-    if (threadIdx.x == 0 && h1[n] == 12345) g1[0] = h2[0];
+  const int rep = blockIdx.x & (kHistRep - 1);
+  unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  for (int b = threadIdx.x; b <= n; b += blockDim.x) {
+    if (h1[b]) atomicAdd(&g1[b], h1[b]);
+    if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
   }
-  if (threadIdx.x == 0) atomicAdd(&v.s2[slot], red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    atomicAdd(&v.s2[slot], t);
+  }
+}
+
+size_t hist_lds_bytes(int ncand, int bits) {
+  const int qmax = 1 << (bits - 1);
+  return (size_t)(ncand + 1) * 8 + (size_t)((ncand + 1 + 3) & ~3) * 4 + (size_t)(qmax + 1) * ncand * 4;
 }
 
 // One wave per job. Lane l owns the consecutive candidate block [l*P, l*P+P) with
@@ -157,8 +182,14 @@ __global__ __launch_bounds__(64) void k_mse_select(const ProbDesc* __restrict__ 
   }
   constexpr int PMAX = (kMaxStage1 + 63) / 64;
   const int P = (n + 63) / 64;
-  const unsigned long long* g1 = v.h1 + (size_t)slot * (n + 1);
-  const unsigned long long* g2 = v.h2 + (size_t)slot * (n + 1);
+  const unsigned long long* g1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
+  const unsigned long long* g2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
+  auto hsum = [&](const unsigned long long* g, int b) {
+    unsigned long long t = 0ull;
+#pragma unroll
+    for (int r = 0; r < kHistRep; ++r) t += g[r * (n + 1) + b];
+    return t;
+  };
   // T(c) = sum_{b > c} h[b]: lane-local suffix over its block, then across lanes
   unsigned long long t1[PMAX], t2[PMAX];
   unsigned long long r1 = 0ull, r2 = 0ull;
@@ -166,7 +197,7 @@ __global__ __launch_bounds__(64) void k_mse_select(const ProbDesc* __restrict__ 
   for (int j = PMAX - 1; j >= 0; --j) {
     t1[j] = r1; t2[j] = r2;                       // exclusive within the lane: b > c
     const int b = lane * P + j;
-    if (j < P && b <= n) { r1 += g1[b]; r2 += g2[b]; }
+    if (j < P && b <= n) { r1 += hsum(g1, b); r2 += hsum(g2, b); }
   }
   // candidates above this lane's block contribute sum of later lanes' blocks, plus b = n
   // when it is not inside any block (n == 64 P exactly).
@@ -179,7 +210,7 @@ __global__ __launch_bounds__(64) void k_mse_select(const ProbDesc* __restrict__ 
   }
   unsigned long long above1 = __shfl_down(s1, 1), above2 = __shfl_down(s2v, 1);
   if (lane == 63) { above1 = 0ull; above2 = 0ull; }
-  if (64 * P == n) { above1 += g1[n]; above2 += g2[n]; }   // b = n lies past every block
+  if (64 * P == n) { above1 += hsum(g1, n); above2 += hsum(g2, n); }   // b = n lies past every block
   const int qmax = 1 << (bits - 1);
   const float denf = (float)(2 * qmax - 1);
   int emx;
@@ -268,15 +299,9 @@ __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d,
 
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s) {
-  static const int var = [] {
-    const char* e = getenv("ADMMQ_HIST_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
   if (nchunks <= 0) return;
-  if (var == 1) hipLaunchKernelGGL(k_mse_hist<1>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
-  else if (var == 2) hipLaunchKernelGGL(k_mse_hist<2>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
-  else if (var == 3) hipLaunchKernelGGL(k_mse_hist<3>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
-  else hipLaunchKernelGGL(k_mse_hist<0>, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  hipLaunchKernelGGL(k_mse_hist, dim3(nchunks), dim3(1024), hist_lds_bytes(ncand, bits), s, d, q, chunks, ncand, bits,
+                     slot);
 }
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s) {

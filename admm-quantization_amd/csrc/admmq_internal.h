@@ -39,6 +39,7 @@ struct MseView {
   unsigned long long* h2;      // [slot][kHistRep][ncand+1]
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
+  float* thr;                  // [2^(kMaxStage1Bits-1)+1][ncand] level thresholds (current iteration)
   const int* done;             // early-exit flag (ADMM) or nullptr
 };
 
@@ -99,6 +100,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
+void launch_mse_prep(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s);
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,

@@ -88,6 +88,7 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.h2 = cv.take<unsigned long long>((size_t)nslot * kHistRep * (ncand + 1));
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
+  v.thr = cv.take<float>((size_t)((1 << (kMaxStage1Bits - 1)) + 1) * ncand);
 }
 
 struct AdmmPlan {
@@ -146,13 +147,18 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
+  // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
+  // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
   std::vector<GemmTile> small;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     const int bm = d.Ip == 32 ? 32 : 64;
     std::vector<GemmTile>& dst = d.Ip == 32 ? small : pl.tiles;
-    for (int tm = 0; tm < d.Ip / bm; ++tm)
-      for (int tn = 0; tn < (d.ld + 63) / 64; ++tn) dst.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
+    const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
+    for (int g0 = 0; g0 < TN; g0 += 8)
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn) dst.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
   }
   pl.ntiles_big = (int)pl.tiles.size();
   pl.ntiles_small = (int)small.size();
@@ -272,7 +278,10 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
   if (qscheme == kMse) {
     const bool all = exhaustive || !two_stage_ok(ncand, bits);
-    if (!all) launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    if (!all) {
+      launch_mse_prep(nullptr, pl.d_jobs, n, ncand, bits, 0, s);
+      launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    }
     launch_mse_select(nullptr, pl.d_jobs, n, ncand, bits, 0, all ? 1 : 0, s);
     launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
   }
@@ -373,7 +382,10 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
-      if (!exhaustive) launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      if (!exhaustive) {
+        launch_mse_prep(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, s);
+        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      }
       launch_mse_select(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, exhaustive ? 1 : 0, s);
       launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       prof_mark(s);

@@ -52,6 +52,24 @@ __device__ float level_threshold(float s, int k) {
   return a;
 }
 
+// Per job and iteration: thr[k][c] for k = 1..qmax, c < n into global memory (one
+// block per job; every stage-1 block then just copies the table into LDS).
+__global__ __launch_bounds__(256) void k_mse_prep(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                  int ncand, int bits, int slot) {
+  const MseView& v = mview(d, qj, blockIdx.x);
+  if (v.done && *v.done) return;
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) return;
+  const int n = ncand;
+  const int qmax = 1 << (bits - 1);
+  const float den = (float)(2 * qmax - 1);
+  for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
+    const int k = 1 + e / n, c = e - (k - 1) * n;
+    const float s = (2.0f * cand_t(mx, c, n)) / den;
+    v.thr[k * n + c] = level_threshold(s, k);
+  }
+}
+
 // Stage 1. thr[k][c] turns every breakpoint probe into one compare:
 // |q_c(x)| >= k  <=>  |x| >= thr[k][c]  (thr increasing in c and in k).
 // 1024 threads x 4 elements per block; the block's histograms are flushed into one of
@@ -71,11 +89,7 @@ __global__ __launch_bounds__(1024) void k_mse_hist(const ProbDesc* __restrict__ 
   float* thr = reinterpret_cast<float*>(h2 + ((n + 1 + 3) & ~3));                 // [qmax+1][n]
   __shared__ double red[16];
   const float den = (float)(2 * qmax - 1);
-  for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
-    const int k = 1 + e / n, c = e - (k - 1) * n;
-    const float s = (2.0f * cand_t(mx, c, n)) / den;
-    thr[k * n + c] = level_threshold(s, k);
-  }
+  for (int e = n + threadIdx.x; e < (qmax + 1) * n; e += blockDim.x) thr[e] = v.thr[e];
   for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
   __syncthreads();
   const float S0 = (float)(0.2 * (double)mx);
@@ -302,6 +316,9 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
   if (nchunks <= 0) return;
   hipLaunchKernelGGL(k_mse_hist, dim3(nchunks), dim3(1024), hist_lds_bytes(ncand, bits), s, d, q, chunks, ncand, bits,
                      slot);
+}
+void launch_mse_prep(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(k_mse_prep, dim3(njobs), dim3(256), 0, s, d, q, ncand, bits, slot);
 }
 void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
                        hipStream_t s) {

@@ -2,7 +2,8 @@
 //
 // Memory layout in HBM (per ADMM problem = one (layer, mode) factor):
 //   Fp, H, U, P, X, HT : float32 [Ip x ld] row-major, ld = roundup(R,32),
-//                        Ip = 32 if I <= 32 else roundup(I,64); pads kept at exactly 0
+//                        Ip = 32 if I <= 32 else roundup(I, 32 WM) (WM = big GEMM tile rows / 32);
+//                        pads kept at exactly 0
 //   M                  : float32 [ldm x ldm], ldm = roundup(R,64); (G+rho I)^-1,
 //                        symmetric, zero outside the R x R block
 //   A64, L64           : float64 [ldm x ldm] SPD factor / inverse-factor scratch
@@ -39,8 +40,9 @@ struct MseView {
   unsigned long long* h2;      // [slot][kHistRep][ncand+1]
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
-  float* thr;                  // [2^(kMaxStage1Bits-1)+1][ncand] level thresholds (current iteration)
+  unsigned* ticket;            // [slot] stage-1 blocks finished (the last one runs the selection)
   const int* done;             // early-exit flag (ADMM) or nullptr
+  int nhist, pad_;             // stage-1 blocks of this job
 };
 
 struct ProbDesc {
@@ -94,15 +96,16 @@ void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
 void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, int slot, int iter,
-                 float eps, int ncand, hipStream_t s);
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
+                 int slot, int iter, float eps, int ncand, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
-void launch_mse_prep(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s);
-void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
-                       hipStream_t s);
+int copy_gemm_trace(unsigned long long* host, int n);
+int gemm_big_wm();
+int copy_hist_trace(unsigned long long* host, int n);
+void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);
 void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits,

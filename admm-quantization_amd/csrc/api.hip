@@ -88,7 +88,7 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.h2 = cv.take<unsigned long long>((size_t)nslot * kHistRep * (ncand + 1));
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
-  v.thr = cv.take<float>((size_t)((1 << (kMaxStage1Bits - 1)) + 1) * ncand);
+  v.ticket = cv.take<unsigned>((size_t)nslot);
 }
 
 struct AdmmPlan {
@@ -100,6 +100,7 @@ struct AdmmPlan {
   Chunk* d_sse = nullptr;
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
+  unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
   int ntiles_big = 0, ntiles_small = 0;
@@ -120,7 +121,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, 64);
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, 32 * gemm_big_wm());
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -142,7 +143,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
   }
   // GEMM tiles, longest K first (LPT over the grid); `first` marks tile (0,0).
-  // 64x64 tiles (Ip > 32) first, then the 32x64 tiles of the thin (I <= 32) factors.
+  // (32 WM)x64 tiles (Ip > 32) first, then the 32x64 tiles of the thin (I <= 32) factors.
   pl.tiles.clear();
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
@@ -153,7 +154,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<GemmTile> small;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
-    const int bm = d.Ip == 32 ? 32 : 64;
+    const int bm = d.Ip == 32 ? 32 : 32 * gemm_big_wm();
     std::vector<GemmTile>& dst = d.Ip == 32 ? small : pl.tiles;
     const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
     for (int g0 = 0; g0 < TN; g0 += 8)
@@ -172,12 +173,14 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     const long long tot = (long long)d.I * d.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.fin_chunks.push_back({i, (int)e});
     for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
+    pl.desc[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
+  pl.d_queue = cv.take<unsigned>(2);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
 }
@@ -243,6 +246,7 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
     for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
     for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
     for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
+    pl.jobs[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
   pl.d_jobs = cv.take<QJob>(n);
   pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
@@ -259,6 +263,7 @@ __global__ void k_qinit(QJob* jobs, int n, int ncand) {
   if (threadIdx.x == 0) {
     v.stat[0] = 0u; v.stat[1] = 0xFFFFFFFFu; v.stat[2] = 0u; v.stat[3] = 0u;
     v.s2[0] = 0.0;
+    v.ticket[0] = 0u;
   }
 }
 
@@ -278,11 +283,8 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
   if (qscheme == kMse) {
     const bool all = exhaustive || !two_stage_ok(ncand, bits);
-    if (!all) {
-      launch_mse_prep(nullptr, pl.d_jobs, n, ncand, bits, 0, s);
-      launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
-    }
-    launch_mse_select(nullptr, pl.d_jobs, n, ncand, bits, 0, all ? 1 : 0, s);
+    if (!all) launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    else launch_mse_select_all(nullptr, pl.d_jobs, n, ncand, 0, s);
     launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
   }
   if (final_pass) launch_qfinal(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), ncand, bits, qscheme, s);
@@ -372,21 +374,19 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   hipStream_t s = static_cast<hipStream_t>(stream);
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
+  if (hipMemsetAsync(pl.d_queue, 0, 2 * sizeof(unsigned), s) != hipSuccess) return check_hip("queue reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);
-    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, slot, it, eps, num_attempts, s);
+    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, slot, it, eps, num_attempts, s);
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
-      if (!exhaustive) {
-        launch_mse_prep(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, s);
-        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
-      }
-      launch_mse_select(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, exhaustive ? 1 : 0, s);
+      if (!exhaustive) launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      else launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
       launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       prof_mark(s);
     }
@@ -398,6 +398,10 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   if (info) hipLaunchKernelGGL(k_export_info, dim3((nprob + 63) / 64), dim3(64), 0, s, pl.d_desc, nprob, info);
   return check_hip("admm_run");
 }
+
+// diagnostics (not in include/admmq.h): per-workgroup timeline of the last GEMM launch
+int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
+int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
                                      int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,

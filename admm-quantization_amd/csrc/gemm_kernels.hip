@@ -3,24 +3,38 @@
 // active (layer, mode) problem. P is produced by the previous iteration's
 // finalize kernel; M is symmetric, so the B operand is read as rows of M.
 //
-// Tile (32*WM) x 64 per workgroup of 2*WM waves; wave (wm, wn) owns the 32 x 32
-// sub-tile at (32 wm, 32 wn) with one v_mfma_f32_32x32x2_f32 accumulator chain
-// (16 accumulator registers). WM = 2 (64 x 64 tiles, 256 threads) for factors with
-// I > 32, WM = 1 (32 x 64, 128 threads) for the 9-row mode-C factors.
-// K-step 32 = 16 MFMAs per wave between barriers, double-buffered through LDS with
-// register prefetch of the next K-step. The LDS images keep k permuted as
-// [row][h][m] (k = 2m + h) so a lane's 16 operands for a K-step are 64 contiguous
-// bytes (4 x ds_read_b128); rows padded to 144 B (conflict-free b128 reads).
+// Tile (32*WM) x 64 per workgroup of 2*WM*KS waves; the KS waves (ks, wm, wn) own the
+// 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
+// chain over its 1/KS slice of every K-step, summed in fixed order through LDS at the
+// end. WM = 2 (64 x 64 tiles) for factors with I > 32, WM = 1 (32 x 64) for the 9-row
+// mode-C factors.
+//
+// Staging: K-step 32 (128 B per operand row). Both operands go global -> LDS by
+// global_load_lds_dwordx4 (no VGPR round trip) into an NS-deep ring of stages, NS-1
+// K-steps in flight; each wave waits with a counted vmcnt for its own pieces of the
+// stage it is about to read and a raw s_barrier publishes the stage (a __syncthreads
+// would drain every in-flight load). A stage image is row-major, 128 B per row, with
+// the 16-B chunk c of row r stored at chunk position c ^ ((r >> 1) & 7) - applied on
+// the global source address, since an LDS-DMA writes lane-linear - so the fragment
+// reads (ds_read_b128) are bank-conflict free for the gfx950 b128 lane groups.
+// The k-order inside a K-step is k = 16 h + m (lane half h, MFMA m): a lane's 16
+// operands are 64 contiguous bytes; A and B use the same order, so the product is
+// exact in any order and only the f32 rounding sequence differs.
 //
 // Epilogue: store HT, X = HT - U, and fold max|X|, min X, max X of the valid
 // region into the problem's per-iteration stat slot (one atomic each per block).
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
 #include "quant_device.h"
 
 namespace admmq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BN = 64, BK = 32, LROW = 36;  // LDS row = 32 floats + 4 pad
+constexpr int BN = 64, BK = 32;
 
 __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_prev, int iter, float eps) {
   if (iter == 0) return false;
@@ -30,137 +44,279 @@ __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_pre
   return (rr < (double)eps) && (ss < (double)eps);
 }
 
-template <int WM>
-__global__ __launch_bounds__(128 * WM) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
-                                                   int slot, int iter, float eps, int ncand) {
-  constexpr int BM = 32 * WM;
-  constexpr int NT = 128 * WM;                 // threads
-  constexpr int AV = BM * (BK / 4) / NT;       // float4 loads of A per thread per K-step (= 2)
-  constexpr int BV = BN * (BK / 4) / NT;       // float4 loads of B per thread per K-step (= 4 / WM)
-  const GemmTile tl = tiles[blockIdx.x];
-  const ProbDesc& p = probs[tl.prob];
-  if (p.flags[0]) return;
-  if (converged_before(p, slot ^ 1, iter, eps)) {
-    if (tl.first && threadIdx.x == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
-    return;
-  }
-  if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
-    unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
-    unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
-    unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
-    for (int c = threadIdx.x; c < ncand; c += NT) sse[c] = 0ull;
-    for (int c = threadIdx.x; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
-    if (threadIdx.x == 0) p.mv.s2[slot] = 0.0;
-  }
+// 16 B per lane global -> LDS (global_load_lds_dwordx4): LDS bytes [lds + 16 lane, +16).
+// The builtin exists only for the device pass (its LDS pointer type does not form on
+// the host, and a template kernel using it would silently lose its host launch stub).
+__device__ __forceinline__ void glds16(const float* g, float* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0);
+#endif
+}
 
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LROW];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LROW];
+// Per-tile timeline of the last GEMM launch (diagnostics: admmq_debug_gemm_trace):
+// {start, end} s_memrealtime ticks (100 MHz) and {workgroup, xcc, hw_id}.
+constexpr int kTraceMax = 8192;
+__device__ unsigned long long g_gemm_trace[kTraceMax][3];
+
+// Workgroup barrier that is also a compiler barrier for memory operations (the builtin
+// s_barrier is not: LDS reads of the next stage could be hoisted above it) and adds
+// no waitcnt of its own (unlike __syncthreads, which would drain in-flight glds).
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their no-wait maxima), gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Grouped GEMM over a tile queue. gridDim.x workgroups take tiles in LPT order
+// (longest K first, as listed in `tiles`): the first tile of a workgroup is its
+// blockIdx, later ones come from a device-scope ticket counter drawn when the
+// workgroup's K-loop ends. Every launch draws exactly ntiles tickets (each workgroup's
+// last draw fails), so launch number `iter` of a run owns tickets
+// [iter * ntiles, (iter + 1) * ntiles) and the counter is zeroed once per run. With
+// gridDim.x == ntiles (the default) every workgroup runs exactly one tile.
+//
+// Workgroup tile (32 WM) x 64 with 2 WM KS waves: the KS waves (ks, wm, wn) own the
+// 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
+// chain over its 1/KS slice of the k range of every K-step; the partials are summed in
+// fixed order at the end.
+template <int WM, int KS, int NS>
+__global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
+                                                        int ntiles, unsigned* __restrict__ queue, int slot, int iter,
+                                                        float eps, int ncand) {
+  constexpr int BM = 32 * WM;
+  constexpr int NSUB = 2 * WM;                 // 32 x 32 sub-tiles per workgroup
+  constexpr int NW = NSUB * KS;                // waves
+  constexpr int NT = 64 * NW;
+  constexpr int ROWS = BM + BN;                // image rows per stage (A then B)
+  constexpr int STAGE = ROWS * 32;             // floats per stage
+  constexpr int NG = ROWS / 8;                 // glds wave-instructions per stage (8 rows each)
+  constexpr int GPW = NG / NW;                 // ... per wave
+  constexpr int QS = 4 / KS;                   // b128 fragment reads per operand per wave per K-step
+  static_assert(KS == 1 || (KS - 1) * NSUB * 1024 <= STAGE, "split-K partials fit in one stage");
+  static_assert(NG % NW == 0, "stage rows must split evenly over the waves");
+  static_assert(KS == 1 || KS == 2 || KS == 4, "KS");
+  static_assert(NS >= 2 && NS <= 6 && GPW * (NS - 2) < 64, "NS");
+
+  // one __shared__ object per stage: the compiler then sees that a stage being read is
+  // not the one being filled and does not drain the in-flight loads before the reads
+  __shared__ __attribute__((aligned(16))) float st0[STAGE];
+  __shared__ __attribute__((aligned(16))) float st1[STAGE];
+  __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float st3[NS > 3 ? STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float st4[NS > 4 ? STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float st5[NS > 5 ? STAGE : 4];
+  float* const stp[6] = {st0, st1, st2, st3, st4, st5};
+  __shared__ int s_next;
+  __shared__ unsigned red[3][NSUB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave / 2, wn = wave & 1;
-  const int ld = p.ld, ldm = p.ldm;
-  const int row0 = tl.tm * BM, col0 = tl.tn * BN;
-  const float* __restrict__ P = p.P;
-  const float* __restrict__ M = p.M;
-
-  // staging: element v of thread t covers row (t + v*NT) / 8, k-quad (t % 8)
-  const int kq = tid & 7;
-  const int r0 = tid >> 3;
-  float4 ra[AV], rb[BV];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v)
-      ra[v] = *reinterpret_cast<const float4*>(P + (size_t)(row0 + r0 + v * (NT / 8)) * ld + k0 + 4 * kq);
-#pragma unroll
-    for (int v = 0; v < BV; ++v)
-      rb[v] = *reinterpret_cast<const float4*>(M + (size_t)(col0 + r0 + v * (NT / 8)) * ldm + k0 + 4 * kq);
-  };
-  auto sstore = [&](int b) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      float* a = &As[b][(r0 + v * (NT / 8)) * LROW + 2 * kq];
-      *reinterpret_cast<float2*>(a) = make_float2(ra[v].x, ra[v].z);
-      *reinterpret_cast<float2*>(a + 16) = make_float2(ra[v].y, ra[v].w);
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      float* bb = &Bs[b][(r0 + v * (NT / 8)) * LROW + 2 * kq];
-      *reinterpret_cast<float2*>(bb) = make_float2(rb[v].x, rb[v].z);
-      *reinterpret_cast<float2*>(bb + 16) = make_float2(rb[v].y, rb[v].w);
-    }
-  };
-
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-
+  const int sub = wave % NSUB, ks = wave / NSUB;
+  const int wm = sub / 2, wn = sub & 1;
   const int i = lane & 31, h = lane >> 5;
-  const int nk = ld / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-    const float4* ap = reinterpret_cast<const float4*>(&As[cur][(32 * wm + i) * LROW + 16 * h]);
-    const float4* bp = reinterpret_cast<const float4*>(&Bs[cur][(32 * wn + i) * LROW + 16 * h]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a = ap[q], b = bp[q];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
+  const int swz = (i >> 1) & 7;
+  const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * wn + i) * 32;
+  const unsigned base = (unsigned)iter * (unsigned)ntiles;
 
-  // epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-  const int col = col0 + 32 * wn + i;
-  unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
-  if (col < ld) {
+  for (int t = blockIdx.x; t < ntiles;) {
+    const unsigned long long t_tile = __builtin_amdgcn_s_memrealtime();
+    const GemmTile tl = tiles[t];
+    const ProbDesc& p = probs[tl.prob];
+    bool skip = p.flags[0] != 0;
+    if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
+      if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
+      skip = true;
+    }
+    if (skip && tid == 0) s_next = (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+    if (!skip) {
+      if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+        unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
+        unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
+        unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
+        for (int c = tid; c < ncand; c += NT) sse[c] = 0ull;
+        for (int c = tid; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
+        if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
+      }
+      const int ld = p.ld, ldm = p.ldm;
+      const int row0 = tl.tm * BM, col0 = tl.tn * BN;
+      const int nk = ld / BK;
+
+      // per-lane global source of each of this wave's glds pieces (K-step 0)
+      const float* src[GPW];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const size_t off = (size_t)row * ld + col;
-      const float ht = acc[r];
-      const float x = ht - p.U[off];
-      p.HT[off] = ht;
-      p.X[off] = x;
-      if (row < p.I && col < p.R) {
-        amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
-        const unsigned e = enc_ord(x);
-        mn = min(mn, e);
-        mxo = max(mxo, e);
+      for (int j = 0; j < GPW; ++j) {
+        const int g = wave * GPW + j;
+        const int r = 8 * g + (lane >> 3);                       // image row
+        const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+        src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + 4 * c
+                          : p.M + (size_t)(col0 + r - BM) * ldm + 4 * c;
+      }
+#define ADMMQ_ISSUE(s, kt)                                                 \
+  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
+    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
+
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+      // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
+      // stages stay in flight), publish it (barrier), refill the stage consumed one step
+      // ago with K-step kt + NS - 1, multiply. Every step issues exactly GPW loads (past
+      // the end the last K-step is re-read into a stage nobody reads), so the wait count
+      // is one constant and the compiler's own wait tracking stays exact. The main loop
+      // runs whole groups of NS steps (stage static, no branches around the MFMAs, which
+      // would move the accumulators out of AGPRs); the last < NS steps run guarded.
+#define ADMMQ_STEP(s, kt)                                                               \
+  do {                                                                                  \
+    wait_vmcnt<GPW * (NS - 2)>();                                                       \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */ \
+    raw_barrier();                                                                      \
+    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                       \
+    const float* st = stp[s];                                                           \
+    _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                 \
+      const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                              \
+      const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);              \
+      const float4 b = *reinterpret_cast<const float4*>(st + boff + cpos);              \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);               \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);               \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);               \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);               \
+    }                                                                                   \
+  } while (0)
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
+      const int nfull = nk / NS * NS;
+      for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) ADMMQ_STEP(s, kt0 + s);
+      }
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s)
+        if (nfull + s < nk) ADMMQ_STEP(s, nfull + s);
+#undef ADMMQ_STEP
+#undef ADMMQ_ISSUE
+      // next ticket, drawn once this tile's K-loop is done (its latency hides behind
+      // the epilogue; drawing earlier would hand tiles out before workers are free)
+      if (tid == 0) s_next = (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+      __syncthreads();   // nothing in flight any more; the stages may be reused
+      if (KS > 1) {      // fixed-order reduction of the KS partial accumulators (deterministic)
+        if (ks > 0) {
+          float* dst = st0 + ((ks - 1) * NSUB + sub) * 1024;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
+        }
+        __syncthreads();
+        if (ks == 0) {
+#pragma unroll
+          for (int j = 1; j < KS; ++j) {
+            const float* s2 = st0 + ((j - 1) * NSUB + sub) * 1024;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += s2[r * 64 + lane];
+          }
+        }
+      }
+
+      // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+      if (ks == 0) {
+        const int col = col0 + 32 * wn + i;
+        unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+        if (col < ld) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const size_t off = (size_t)row * ld + col;
+            const float ht = acc[r];
+            const float x = ht - p.U[off];
+            p.HT[off] = ht;
+            p.X[off] = x;
+            if (row < p.I && col < p.R) {
+              amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
+              const unsigned e = enc_ord(x);
+              mn = min(mn, e);
+              mxo = max(mxo, e);
+            }
+          }
+        }
+        amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
+        if (lane == 0) { red[0][sub] = amax; red[1][sub] = mn; red[2][sub] = mxo; }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
+#pragma unroll
+        for (int w = 1; w < NSUB; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
+        unsigned* st = p.mv.stat + 4 * slot;
+        atomicMax(&st[0], a0);
+        atomicMin(&st[1], a1);
+        atomicMax(&st[2], a2);
       }
     }
-  }
-  amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
-  __shared__ unsigned red[3][2 * WM];
-  if (lane == 0) { red[0][wave] = amax; red[1][wave] = mn; red[2][wave] = mxo; }
-  __syncthreads();
-  if (tid == 0) {
-#pragma unroll
-    for (int w = 1; w < 2 * WM; ++w) {
-      red[0][0] = max(red[0][0], red[0][w]); red[1][0] = min(red[1][0], red[1][w]); red[2][0] = max(red[2][0], red[2][w]);
+    if (tid == 0 && t < kTraceMax) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+      g_gemm_trace[t][0] = t_tile;
+      g_gemm_trace[t][1] = __builtin_amdgcn_s_memrealtime();
+      g_gemm_trace[t][2] = ((unsigned long long)blockIdx.x << 48) | ((unsigned long long)xcc << 32) | hw;
     }
-    unsigned* st = p.mv.stat + 4 * slot;
-    atomicMax(&st[0], red[0][0]);
-    atomicMin(&st[1], red[1][0]);
-    atomicMax(&st[2], red[2][0]);
+    __syncthreads();   // s_next visible; every wave done with this tile's LDS
+    t = s_next;
+    __syncthreads();   // s_next read by all before the next tile's draw overwrites it
   }
 }
 
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, int slot, int iter,
-                 float eps, int ncand, hipStream_t s) {
-  // tiles[0 .. ntiles_big) are 64x64 (WM=2), then ntiles_small 32x64 tiles (WM=1)
-  if (ntiles_big > 0)
-    hipLaunchKernelGGL(k_gemm<2>, dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
-  if (ntiles_small > 0)
-    hipLaunchKernelGGL(k_gemm<1>, dim3(ntiles_small), dim3(128), 0, s, d, tiles + ntiles_big, slot, iter, eps, ncand);
+int copy_gemm_trace(unsigned long long* host, int n) {
+  n = n < kTraceMax ? n : kTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), (size_t)n * 3 * sizeof(unsigned long long)) == hipSuccess ? n : -1;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+// Row height of the big tiles / 32 (the padded factor height Ip is a multiple of it)
+int gemm_big_wm() {
+  static const int wm = env_int("ADMMQ_GEMM_WM", 2) == 4 ? 4 : 2;
+  return wm;
+}
+
+// Workgroups per CU for the persistent grid (MI355X: 256 CUs)
+static int gemm_grid(int ntiles, int per_cu) { return std::min(ntiles, 256 * per_cu); }
+
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
+                 int slot, int iter, float eps, int ncand, hipStream_t s) {
+  // tiles[0 .. ntiles_big) are (32 WM)x64, then ntiles_small 32x64 tiles (WM=1);
+  // queue[0] / queue[1] are their ticket counters.
+  static const int cfg_big = env_int("ADMMQ_GEMM_BIG", 13);     // KS*10 + NS
+  static const int cfg_small = env_int("ADMMQ_GEMM_SMALL", 24);
+  static const int per_cu = env_int("ADMMQ_GEMM_PER_CU", 0);    // 0: one workgroup per tile
+#define ADMMQ_GEMM(WM, KS, NS, n, t, q)                                                                      \
+  hipLaunchKernelGGL((k_gemm<WM, KS, NS>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, d, \
+                     t, n, q, slot, iter, eps, ncand)
+  if (ntiles_big > 0) {
+    if (gemm_big_wm() == 4) {
+      ADMMQ_GEMM(4, 1, 3, ntiles_big, tiles, queue);
+    } else {
+      switch (cfg_big) {
+        case 14: ADMMQ_GEMM(2, 1, 4, ntiles_big, tiles, queue); break;
+        case 23: ADMMQ_GEMM(2, 2, 3, ntiles_big, tiles, queue); break;
+        case 12: ADMMQ_GEMM(2, 1, 2, ntiles_big, tiles, queue); break;
+        default: ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles, queue); break;
+      }
+    }
+  }
+  if (ntiles_small > 0) {
+    const GemmTile* t = tiles + ntiles_big;
+    switch (cfg_small) {
+      case 14: ADMMQ_GEMM(1, 1, 4, ntiles_small, t, queue + 1); break;
+      default: ADMMQ_GEMM(1, 2, 4, ntiles_small, t, queue + 1); break;
+    }
+  }
+#undef ADMMQ_GEMM
 }
 
 }  // namespace admmq

@@ -14,9 +14,14 @@
 //                       S = {c : A - E <= min(A + E)} provably holds the argmin.
 // stage 2  k_mse_sse    canonical SSE only for c in S (|S| = 1 almost always: then the
 //                       kernel exits at once); exhaustive when |S| > kMaxSel or forced.
+#include <algorithm>
+#include <cstdlib>
+
 #include "quant_device.h"
 
 namespace admmq {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;   // global (not flat) sc1 loads
 
 __device__ __forceinline__ const MseView& mview(const ProbDesc* d, const QJob* q, int job) {
   return d ? d[job].mv : q[job].mv;
@@ -52,95 +57,227 @@ __device__ float level_threshold(float s, int k) {
   return a;
 }
 
-// Per job and iteration: thr[k][c] for k = 1..qmax, c < n into global memory (one
-// block per job; every stage-1 block then just copies the table into LDS).
-__global__ __launch_bounds__(256) void k_mse_prep(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                  int ncand, int bits, int slot) {
-  const MseView& v = mview(d, qj, blockIdx.x);
-  if (v.done && *v.done) return;
-  const float mx = __uint_as_float(v.stat[4 * slot]);
-  if (mse_degenerate(mx)) return;
-  const int n = ncand;
-  const int qmax = 1 << (bits - 1);
+// Per-block phase timeline of the last stage-1 launch (diagnostics, admmq_debug_hist_trace):
+// s_memrealtime at {start, thresholds ready, elements done, flushed, end}, and the CU id.
+constexpr int kHistTraceMax = 8192;
+__device__ unsigned long long g_hist_trace[kHistTraceMax][6];
+
+int copy_hist_trace(unsigned long long* host, int n) {
+  n = n < kHistTraceMax ? n : kHistTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hist_trace), (size_t)n * 6 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
+
+// Threshold table of one job into LDS: thr[(k-1) n + c] = smallest a with
+// |q_c(a)| >= k, for k = 1..qmax (increasing in c and in k).
+__device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax) {
   const float den = (float)(2 * qmax - 1);
   for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
     const int k = 1 + e / n, c = e - (k - 1) * n;
-    const float s = (2.0f * cand_t(mx, c, n)) / den;
-    v.thr[k * n + c] = level_threshold(s, k);
+    thr[e] = level_threshold((2.0f * cand_t(mx, c, n)) / den, k);
   }
 }
 
-// Stage 1. thr[k][c] turns every breakpoint probe into one compare:
-// |q_c(x)| >= k  <=>  |x| >= thr[k][c]  (thr increasing in c and in k).
+__device__ __forceinline__ int hist_fixed_exp(float mx, long long nelem, int qmax) {
+  int emx;
+  (void)__builtin_frexpf(mx, &emx);
+  const long long nterm = nelem * qmax;
+  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
+  return 61 - emx - clt;
+}
+
+// Candidate selection for one job from the summed stage-1 histograms H1/H2 (LDS,
+// n+1 bins) and S2, by one wave. Lane l owns candidates [l P, l P + P), P = ceil(n/64);
+// T(c) = sum_{b>c} H[b] = (later lanes' blocks, wave suffix scan) + (rest of the lane's
+// block, walked downwards). A(c) = S2 - 2 s T1 + s^2 T2 with E(c) its rigorous error
+// bound (oracle/stage1_model.py); pass 1 finds min(A + E), pass 2 writes
+// S = {c : A - E <= min(A + E)} in ascending order (prefix count over lanes).
+struct SelCtx {
+  double S2, fixu, u, Kterm, Nterm, tiny;
+  float mx, denf;
+  int n;
+  __device__ void bounds(int c, unsigned long long T1i, unsigned long long T2i, double& lo, double& hi) const {
+    const double s = (double)((2.0f * cand_t(mx, c, n)) / denf);
+    const double T1 = (double)T1i * fixu;
+    const double T2 = (double)T2i;
+    const double A = S2 - 2.0 * s * T1 + s * s * T2;
+    const double mag = S2 + 2.0 * s * T1 + s * s * T2;
+    const double slack = 1e-10 * mag;
+    const double sh = fmax(A, 0.0) + slack;
+    const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
+    const double E = B1 + 3.0000002 * u * (sh + B1) + Kterm + 2.0 * s * Nterm * fixu + slack + tiny;
+    lo = A - E;
+    hi = A + E;
+  }
+};
+
+__device__ void select_wave(const MseView& v, int* sel, const unsigned long long* H1, const unsigned long long* H2,
+                            double S2, float mx, int n, int qmax) {
+  const int lane = threadIdx.x & 63;
+  const int P = (n + 63) / 64;
+  const int c0 = lane * P, c1 = min(c0 + P, n);   // this lane's candidates [c0, c1)
+  unsigned long long r1 = 0ull, r2 = 0ull;
+  for (int b = c0; b < c1; ++b) { r1 += H1[b]; r2 += H2[b]; }
+  unsigned long long s1 = r1, s2v = r2;          // inclusive suffix scan over lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o1 = __shfl_down(s1, off);
+    const unsigned long long o2 = __shfl_down(s2v, off);
+    if (lane + off < 64) { s1 += o1; s2v += o2; }
+  }
+  unsigned long long above1 = __shfl_down(s1, 1), above2 = __shfl_down(s2v, 1);
+  if (lane == 63) { above1 = 0ull; above2 = 0ull; }
+  above1 += H1[n]; above2 += H2[n];               // b = n lies past every candidate
+  SelCtx cx;
+  cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * qmax - 1);
+  cx.u = 0x1p-24;
+  cx.fixu = ldexp(1.0, -hist_fixed_exp(mx, v.nelem, qmax));
+  cx.Kterm = (double)v.nq * ldexp(1.0, -fixed_exp(mx, v.nq));
+  cx.Nterm = (double)((long long)v.nelem * qmax);
+  cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
+  double mymin = 1e300;
+  {
+    unsigned long long t1 = above1, t2 = above2;
+    for (int c = c1 - 1; c >= c0; --c) {
+      double lo, hi;
+      cx.bounds(c, t1, t2, lo, hi);
+      mymin = fmin(mymin, hi);
+      t1 += H1[c]; t2 += H2[c];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mymin = fmin(mymin, __shfl_xor(mymin, off));
+  unsigned long long keep = 0ull;                  // bit (c - c0) set: c in S (P <= 16)
+  int cnt = 0;
+  {
+    unsigned long long t1 = above1, t2 = above2;
+    for (int c = c1 - 1; c >= c0; --c) {
+      double lo, hi;
+      cx.bounds(c, t1, t2, lo, hi);
+      if (lo <= mymin) { keep |= 1ull << (c - c0); ++cnt; }
+      t1 += H1[c]; t2 += H2[c];
+    }
+  }
+  int pre = cnt;                                   // inclusive prefix over lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(pre, off);
+    if (lane >= off) pre += o;
+  }
+  const int total = __shfl(pre, 63);
+  int pos = pre - cnt;
+  for (int c = c0; c < c1; ++c) {
+    if ((keep >> (c - c0)) & 1ull) {
+      if (pos < kMaxSel) sel[2 + pos] = c;
+      ++pos;
+    }
+  }
+  if (lane == 0) {   // sel = {|S| (n: exhaustive), unused, S ascending...}; |S| == 1 -> c* = sel[2]
+    if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
+    else { sel[0] = total; sel[1] = 0; }
+  }
+}
+
+// Stage 1. Each element x (a = |x|) has level k reached by candidate c iff
+// a >= thr[k][c]; levels k <= kfull are reached by every candidate (b_k = n, summed
+// in registers), levels kfull < k <= k0 have a breakpoint b_k in [1, n-1]: a linear
+// estimate from t_c ~ S0 + c step (off by at most one) checked against the two
+// neighbouring thresholds (one ds_read2), corrected, and re-verified in a rare slow
+// path. QMAX = 2^(bits-1) is a template argument so the level loop unrolls and the
+// LDS reads of all levels of an element are in flight together.
 // 1024 threads x 4 elements per block; the block's histograms are flushed into one of
-// kHistRep replicas of the job's global histograms (replica = block % kHistRep).
-__global__ __launch_bounds__(1024) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                   const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
+// kHistRep replicas of the job's global histograms; the last block of the job to
+// finish (ticket) sums the replicas and runs the candidate selection.
+template <int QMAX>
+__global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                   const Chunk* __restrict__ chunks, int ncand, int slot, int abl) {
+  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   const Chunk ck = chunks[blockIdx.x];
   const MseView& v = mview(d, qj, ck.job);
   if (v.done && *v.done) return;
+  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
   const float mx = __uint_as_float(v.stat[4 * slot]);
-  if (mse_degenerate(mx)) return;
+  if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
+    if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = ncand;
-  const int qmax = 1 << (bits - 1);
-  unsigned long long* h1 = reinterpret_cast<unsigned long long*>(smem);          // n+1
-  unsigned* h2 = reinterpret_cast<unsigned*>(h1 + (n + 1));                       // n+1
-  float* thr = reinterpret_cast<float*>(h2 + ((n + 1 + 3) & ~3));                 // [qmax+1][n]
+  const int nb = n + 1 + 64;   // bins 0..n, then one private dummy bin per lane (branch-free atomics)
+  unsigned long long* h1 = reinterpret_cast<unsigned long long*>(smem);          // nb
+  unsigned* h2 = reinterpret_cast<unsigned*>(h1 + nb);                            // nb
+  float* thr = reinterpret_cast<float*>(h2 + ((nb + 3) & ~3));                    // [QMAX][n]
   __shared__ double red[16];
-  const float den = (float)(2 * qmax - 1);
-  for (int e = n + threadIdx.x; e < (qmax + 1) * n; e += blockDim.x) thr[e] = v.thr[e];
-  for (int b = threadIdx.x; b <= n; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
+  __shared__ int last;
+  // this thread's 4 elements: issued first, so the load overlaps the table setup
+  const long long total = (long long)v.rows * v.ld;
+  const long long e = (long long)ck.start + 4LL * threadIdx.x;
+  float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total) x4 = *reinterpret_cast<const float4*>(v.X + e);
+  fill_thresholds(thr, mx, n, QMAX);
+  if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
   __syncthreads();
+  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
   const float S0 = (float)(0.2 * (double)mx);
   const float E0 = (float)(1.2 * (double)mx);
   const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
-  int emx;
-  (void)__builtin_frexpf(mx, &emx);
-  const long long nterm = (long long)v.nelem * qmax;
-  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
-  const int K1 = 61 - emx - clt;
-  const long long total = (long long)v.rows * v.ld;
+  const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
+  const int dummy = n + 1 + (threadIdx.x & 63);
+  float tlo0[QMAX], thin[QMAX];   // per level: thresholds of the first and the last candidate
+#pragma unroll
+  for (int k = 0; k < QMAX; ++k) { tlo0[k] = thr[k * n]; thin[k] = thr[k * n + n - 1]; }
   double s2 = 0.0;
-  // b = n ("level >= k for every candidate") is the most common breakpoint for small
-  // k: accumulate it in registers instead of colliding LDS atomics.
   unsigned long long full1 = 0ull;
   unsigned full2 = 0u;
-  const long long e = (long long)ck.start + 4LL * threadIdx.x;
-  if (e < total) {
-    const float4 x4 = *reinterpret_cast<const float4*>(v.X + e);
-    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+  const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float x = xs[j];
-      if (x == 0.f) continue;
-      s2 += (double)x * (double)x;
-      const float a = __builtin_fabsf(x);
-      const int cap = (x > 0.f) ? qmax - 1 : qmax;
-      int k0 = 0, kfull = 0;
-      for (int k = 1; k <= cap; ++k) {
-        k0 += (a >= thr[k * n]) ? 1 : 0;
-        kfull += (a >= thr[k * n + n - 1]) ? 1 : 0;
-      }
-      if (k0 <= 0) continue;
-      const unsigned long long af = to_fixed(a, K1);
-      if (kfull > 0) {
-        full1 += af * (unsigned long long)kfull;
-        full2 += (unsigned)(kfull * kfull);        // sum_{k<=kfull} (2k-1)
-      }
-      int bprev = n - 1;
-      for (int k = kfull + 1; k <= k0; ++k) {
-        // b_k = #{c : a >= thr[k][c]} in [1, n-1]; estimate from t_c ~ S0 + c*step
-        const float* tk = thr + k * n;
-        const float tau = a * den * __builtin_amdgcn_rcpf((float)(2 * k - 1));   // estimate only
-        const float ce = (tau - S0) * inv_step;
-        int b = (ce >= (float)n) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
-        b = min(max(b, 1), bprev);
-        while (b < n - 1 && a >= tk[b]) ++b;
-        while (b > 1 && a < tk[b - 1]) --b;
-        bprev = b;
-        atomicAdd(&h1[b], af);
-        atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+  for (int j = 0; j < 4; ++j) {
+    const float x = xs[j];
+    s2 += (double)x * (double)x;
+    const float a = __builtin_fabsf(x);
+    const int cap = (x > 0.f) ? QMAX - 1 : QMAX;
+    int k0 = 0, kfull = 0;
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k) {
+      k0 += (k <= cap && a >= tlo0[k - 1]) ? 1 : 0;
+      kfull += (k <= cap && a >= thin[k - 1]) ? 1 : 0;
+    }
+    if (x == 0.f) k0 = 0;
+    const unsigned long long af = to_fixed(a, K1);
+    full1 += af * (unsigned long long)kfull;
+    full2 += (unsigned)(kfull * kfull);              // sum_{k<=kfull} (2k-1)
+    // levels kfull < k <= k0 have a breakpoint b in [1, n-1]: a linear estimate (off by at
+    // most one) checked against its two neighbouring thresholds; exact -> add now (inactive
+    // lanes add 0 to their private dummy bin, no branch); off -> the rare exact search below
+    unsigned slow = 0u;
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k) {
+      const bool act = (k > kfull && k <= k0);
+      const float tau = a * ((float)(2 * QMAX - 1) / (float)(2 * k - 1));   // estimate only
+      const float ce = (tau - S0) * inv_step;
+      int b = (ce >= (float)(n - 1)) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
+      b = max(min(b, n - 1), 1);
+      const float* tk = thr + (k - 1) * n;
+      const bool exact = (a >= tk[b - 1]) && (a < tk[b]);
+      const bool add = act && exact;
+      slow |= (act && !exact) ? (1u << k) : 0u;
+      const int bin = add ? b : dummy;
+      atomicAdd(&h1[bin], add ? af : 0ull);
+      atomicAdd(&h2[bin], add ? (unsigned)(2 * k - 1) : 0u);
+    }
+    if (slow) {   // rare: exact breakpoint by binary search (largest b with thr[k][b-1] <= a)
+#pragma unroll 1
+      for (int k = 1; k <= QMAX; ++k) {
+        if (!((slow >> k) & 1u)) continue;
+        const float* tk = thr + (k - 1) * n;
+        int lo = 1, hi = n - 1;   // a >= tk[0] and a < tk[n-1]: answer in [1, n-1]
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (a >= tk[mid - 1]) lo = mid; else hi = mid - 1;
+        }
+        atomicAdd(&h1[lo], af);
+        atomicAdd(&h2[lo], (unsigned)(2 * k - 1));
       }
     }
   }
@@ -152,181 +289,144 @@ __global__ __launch_bounds__(1024) void k_mse_hist(const ProbDesc* __restrict__ 
   }
   if ((threadIdx.x & 63) == 0) {
     red[threadIdx.x >> 6] = s2;
-    atomicAdd(&h1[n], full1);
-    atomicAdd(&h2[n], full2);
+    if (full1) atomicAdd(&h1[n], full1);
+    if (full2) atomicAdd(&h2[n], full2);
   }
   __syncthreads();
+  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
   const int rep = blockIdx.x & (kHistRep - 1);
-  unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
-  unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  unsigned long long* g1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
+  unsigned long long* g2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
   for (int b = threadIdx.x; b <= n; b += blockDim.x) {
-    if (h1[b]) atomicAdd(&g1[b], h1[b]);
-    if (h2[b]) atomicAdd(&g2[b], (unsigned long long)h2[b]);
+    if (h1[b]) atomicAdd(&g1[rep * (n + 1) + b], h1[b]);
+    if (h2[b]) atomicAdd(&g2[rep * (n + 1) + b], (unsigned long long)h2[b]);
   }
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
     atomicAdd(&v.s2[slot], t);
   }
+  // ticket: the last block of this job to arrive selects the candidate set. Everything
+  // it reads was written by device-scope atomics (performed at the coherence point), so
+  // draining this block's outstanding atomics (vmcnt(0)) orders them before the ticket;
+  // no L2 writeback (a release fence per block costs ~100+ us over the grid).
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = (__hip_atomic_fetch_add(&v.ticket[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(v.nhist - 1)) ? 1 : 0;
+  __syncthreads();
+  const unsigned long long T3 = __builtin_amdgcn_s_memrealtime();
+  auto trace = [&](unsigned long long T4) {
+    if (threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
+      g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = T1; g_hist_trace[blockIdx.x][2] = T2;
+      g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4;
+      g_hist_trace[blockIdx.x][5] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                                    __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    }
+  };
+  if (!last) { trace(T3); return; }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  unsigned long long* H1 = h1;                                            // reuse LDS: n+1 each
+  unsigned long long* H2 = reinterpret_cast<unsigned long long*>(thr);
+  for (int b = threadIdx.x; b <= n; b += blockDim.x) {
+    unsigned long long t1 = 0ull, t2 = 0ull;
+#pragma unroll
+    for (int r = 0; r < kHistRep; ++r) {
+      t1 += __hip_atomic_load((gu64*)&g1[r * (n + 1) + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t2 += __hip_atomic_load((gu64*)&g2[r * (n + 1) + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    H1[b] = t1; H2[b] = t2;
+  }
+  __syncthreads();
+  if ((abl & 16) && threadIdx.x < 64) {   // timing ablation: the selection twice (same result)
+    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    select_wave(v, sel, H1, H2, S2, mx, n, QMAX);
+  }
+  if (threadIdx.x < 64) {
+    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    select_wave(v, sel, H1, H2, S2, mx, n, QMAX);
+  }
+  trace(__builtin_amdgcn_s_memrealtime());
 }
 
 size_t hist_lds_bytes(int ncand, int bits) {
   const int qmax = 1 << (bits - 1);
-  return (size_t)(ncand + 1) * 8 + (size_t)((ncand + 1 + 3) & ~3) * 4 + (size_t)(qmax + 1) * ncand * 4;
+  const size_t nb = (size_t)ncand + 1 + 64;
+  const size_t thr = std::max((size_t)qmax * ncand * 4, (size_t)(ncand + 1) * 8);   // also holds H2 sums
+  return nb * 8 + ((nb + 3) & ~(size_t)3) * 4 + thr;
 }
 
-// One wave per job. Lane l owns the consecutive candidate block [l*P, l*P+P) with
-// P = ceil(n/64): suffix sums come from a per-lane pass plus a wave-level exclusive
-// suffix scan, the set S is built in ascending order from a prefix count over lanes.
-__global__ __launch_bounds__(64) void k_mse_select(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                   int ncand, int bits, int slot, int force_all) {
+// Exhaustive / degenerate path only (stage 1 not run): sel = {n, -1} or {1, 0}.
+__global__ __launch_bounds__(64) void k_mse_select_all(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                       int ncand, int slot) {
   const MseView& v = mview(d, qj, blockIdx.x);
   if (v.done && *v.done) return;
   int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-  const int lane = threadIdx.x;
   const float mx = __uint_as_float(v.stat[4 * slot]);
-  if (mse_degenerate(mx)) {
-    if (lane == 0) { sel[0] = 1; sel[1] = 0; }   // finalize emits NaN for degenerate mx
-    return;
-  }
-  const int n = ncand;
-  if (force_all || n > kMaxStage1) {
-    if (lane == 0) { sel[0] = n; sel[1] = -1; }
-    return;
-  }
-  constexpr int PMAX = (kMaxStage1 + 63) / 64;
-  const int P = (n + 63) / 64;
-  const unsigned long long* g1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
-  const unsigned long long* g2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
-  auto hsum = [&](const unsigned long long* g, int b) {
-    unsigned long long t = 0ull;
-#pragma unroll
-    for (int r = 0; r < kHistRep; ++r) t += g[r * (n + 1) + b];
-    return t;
-  };
-  // T(c) = sum_{b > c} h[b]: lane-local suffix over its block, then across lanes
-  unsigned long long t1[PMAX], t2[PMAX];
-  unsigned long long r1 = 0ull, r2 = 0ull;
-#pragma unroll
-  for (int j = PMAX - 1; j >= 0; --j) {
-    t1[j] = r1; t2[j] = r2;                       // exclusive within the lane: b > c
-    const int b = lane * P + j;
-    if (j < P && b <= n) { r1 += hsum(g1, b); r2 += hsum(g2, b); }
-  }
-  // candidates above this lane's block contribute sum of later lanes' blocks, plus b = n
-  // when it is not inside any block (n == 64 P exactly).
-  unsigned long long s1 = r1, s2v = r2;          // inclusive suffix scan over lanes
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long o1 = __shfl_down(s1, off);
-    const unsigned long long o2 = __shfl_down(s2v, off);
-    if (lane + off < 64) { s1 += o1; s2v += o2; }
-  }
-  unsigned long long above1 = __shfl_down(s1, 1), above2 = __shfl_down(s2v, 1);
-  if (lane == 63) { above1 = 0ull; above2 = 0ull; }
-  if (64 * P == n) { above1 += hsum(g1, n); above2 += hsum(g2, n); }   // b = n lies past every block
-  const int qmax = 1 << (bits - 1);
-  const float denf = (float)(2 * qmax - 1);
-  int emx;
-  (void)__builtin_frexpf(mx, &emx);
-  const long long nterm = (long long)v.nelem * qmax;
-  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
-  const int K1 = 61 - emx - clt;
-  const int K = fixed_exp(mx, v.nq);
-  const double S2 = v.s2[slot];
-  const double u = 0x1p-24;
-  const double fixu = ldexp(1.0, -K1);
-  double lo[PMAX], hi[PMAX];
-  double mymin = 1e300;
-#pragma unroll
-  for (int j = 0; j < PMAX; ++j) {
-    const int c = lane * P + j;
-    lo[j] = 1e300; hi[j] = 1e300;
-    if (j < P && c < n) {
-      const double s = (double)((2.0f * cand_t(mx, c, n)) / denf);
-      const double T1 = (double)(t1[j] + above1) * fixu;
-      const double T2 = (double)(t2[j] + above2);
-      const double A = S2 - 2.0 * s * T1 + s * s * T2;
-      const double mag = S2 + 2.0 * s * T1 + s * s * T2;
-      const double slack = 1e-10 * mag;
-      const double sh = fmax(A, 0.0) + slack;
-      const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
-      const double E = B1 + 3.0000002 * u * (sh + B1) + (double)v.nq * ldexp(1.0, -K) +
-                       2.0 * s * (double)nterm * fixu + slack + 8.0 * (double)v.nelem * 0x1p-149;
-      lo[j] = A - E;
-      hi[j] = A + E;
-      mymin = fmin(mymin, hi[j]);
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) mymin = fmin(mymin, __shfl_xor(mymin, off));
-  int cnt = 0;
-#pragma unroll
-  for (int j = 0; j < PMAX; ++j) cnt += (lo[j] <= mymin) ? 1 : 0;
-  int pre = cnt;                                   // inclusive prefix over lanes
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(pre, off);
-    if (lane >= off) pre += o;
-  }
-  const int total = __shfl(pre, 63);
-  int pos = pre - cnt;
-#pragma unroll
-  for (int j = 0; j < PMAX; ++j) {
-    if (lo[j] <= mymin) {
-      if (pos < kMaxSel) sel[2 + pos] = lane * P + j;
-      ++pos;
-    }
-  }
-  if (lane == 0) {   // sel = {|S| (n: exhaustive), unused, S ascending...}; |S| == 1 -> c* = sel[2]
-    if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
-    else { sel[0] = total; sel[1] = 0; }
+  if (threadIdx.x == 0) {
+    if (mse_degenerate(mx)) { sel[0] = 1; sel[1] = 0; }
+    else { sel[0] = ncand; sel[1] = -1; }
   }
 }
 
+// Stage 2: canonical SSE of the candidates in S (or all) over 512-quad chunks. Only
+// jobs with |S| > 1 have work, so a small grid strides over the chunk list.
 __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                 const Chunk* __restrict__ chunks, int ncand, int bits, int slot) {
-  const Chunk ck = chunks[blockIdx.x];
-  const MseView& v = mview(d, qj, ck.job);
-  if (v.done && *v.done) return;
-  const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-  const int ns = sel[0];
-  if (ns == 1) return;
-  const float mx = __uint_as_float(v.stat[4 * slot]);
-  if (mse_degenerate(mx)) return;
+                                                 const Chunk* __restrict__ chunks, int nchunks, int ncand, int bits,
+                                                 int slot) {
   __shared__ float4 xs[kSseQuads];
   __shared__ int list[kMaxSel];
-  const int nqc = min(kSseQuads, v.nq - ck.start);
-  for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
-    const int qi = ck.start + t;
-    const int row = qi / v.qpr;
-    const int qc = qi - row * v.qpr;
-    xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const Chunk ck = chunks[ci];
+    const MseView& v = mview(d, qj, ck.job);
+    if (v.done && *v.done) continue;
+    const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+    const int ns = sel[0];
+    if (ns == 1) continue;
+    const float mx = __uint_as_float(v.stat[4 * slot]);
+    if (mse_degenerate(mx)) continue;
+    const int nqc = min(kSseQuads, v.nq - ck.start);
+    __syncthreads();   // previous chunk's LDS reads are done
+    for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
+      const int qi = ck.start + t;
+      const int row = qi / v.qpr;
+      const int qc = qi - row * v.qpr;
+      xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+    }
+    const bool all = ns >= ncand;
+    if (!all)
+      for (int j = threadIdx.x; j < ns; j += blockDim.x) list[j] = sel[2 + j];
+    __syncthreads();
+    sse_sweep_list(xs, nqc, mx, fixed_exp(mx, v.nq), ncand, bits, all ? nullptr : list, all ? ncand : ns,
+                   v.sse + (size_t)slot * ncand);
   }
-  const bool all = ns >= ncand;
-  if (!all)
-    for (int j = threadIdx.x; j < ns; j += blockDim.x) list[j] = sel[2 + j];
-  __syncthreads();
-  sse_sweep_list(xs, nqc, mx, fixed_exp(mx, v.nq), ncand, bits, all ? nullptr : list, all ? ncand : ns,
-                 v.sse + (size_t)slot * ncand);
 }
 
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, hipStream_t s) {
   if (nchunks <= 0) return;
-  hipLaunchKernelGGL(k_mse_hist, dim3(nchunks), dim3(1024), hist_lds_bytes(ncand, bits), s, d, q, chunks, ncand, bits,
-                     slot);
+  const size_t lds = hist_lds_bytes(ncand, bits);
+  static const int abl = getenv("ADMMQ_HIST_ABLATE") ? atoi(getenv("ADMMQ_HIST_ABLATE")) : 0;   // timing only
+  switch (bits) {
+    case 1: hipLaunchKernelGGL(k_mse_hist<1>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    case 2: hipLaunchKernelGGL(k_mse_hist<2>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    case 3: hipLaunchKernelGGL(k_mse_hist<4>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    case 4: hipLaunchKernelGGL(k_mse_hist<8>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    case 5: hipLaunchKernelGGL(k_mse_hist<16>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    default: hipLaunchKernelGGL(k_mse_hist<32>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+  }
 }
-void launch_mse_prep(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(k_mse_prep, dim3(njobs), dim3(256), 0, s, d, q, ncand, bits, slot);
-}
-void launch_mse_select(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, int force_all,
-                       hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(k_mse_select, dim3(njobs), dim3(64), 0, s, d, q, ncand, bits, slot, force_all);
+void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(k_mse_select_all, dim3(njobs), dim3(64), 0, s, d, q, ncand, slot);
 }
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s) {
-  if (nchunks > 0) hipLaunchKernelGGL(k_mse_sse, dim3(nchunks), dim3(256), 0, s, d, q, chunks, ncand, bits, slot);
+  if (nchunks > 0)
+    hipLaunchKernelGGL(k_mse_sse, dim3(std::min(nchunks, 512)), dim3(256), 0, s, d, q, chunks, nchunks, ncand, bits,
+                       slot);
 }
 
 }  // namespace admmq

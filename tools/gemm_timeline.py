@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-workgroup timeline of one grouped-GEMM launch (diagnostics).
+
+Runs the resnet18 mode-`--mode` factor problems of the bench workload through
+admm_iteration_batched for a few iterations, then reads the last GEMM launch's
+per-block {start, end, XCC, HW_ID} trace and prints the kernel span, per-CU busy
+time and how blocks were placed."""
+import argparse
+import collections
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "admm-quantization_amd"))
+import torch  # noqa: E402
+from admmq import _lib, synthetic  # noqa: E402
+from admmq.admm import admm_iteration_batched  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--mode", type=int, default=0)
+ap.add_argument("--iters", type=int, default=4)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+g = torch.Generator().manual_seed(0)
+probs = []
+for s in synthetic.resnet18_layers():
+    R = s.rank()
+    I = s.shape[a.mode]
+    B = torch.randn(R, 2 * R, generator=g) / (2 * R) ** 0.5
+    G = (B @ B.T + 0.5 * torch.eye(R)).to(dev)
+    F = torch.randn(I, R, generator=g).to(dev)
+    H = torch.randn(I, R, generator=g).to(dev) * 0.1
+    U = torch.zeros(I, R, device=dev)
+    probs.append((H, U, F, G))
+admm_iteration_batched(probs, a.iters, 0.0, 4, "tensor_mseminmax_symmetric", check_spd=False)
+torch.cuda.synchronize()
+lib = _lib.load()
+lib.admmq_debug_gemm_trace.restype = ctypes.c_int32
+n = 8192
+buf = (ctypes.c_ulonglong * (3 * n))()
+got = lib.admmq_debug_gemm_trace(buf, n)
+recs = []
+for b in range(got):
+    t0, t1, hid = buf[3 * b], buf[3 * b + 1], buf[3 * b + 2]
+    if t0 == 0 or t1 < t0:
+        break
+    wg = hid >> 48
+    xcc = (hid >> 32) & 0xFFFF
+    hw = hid & 0xFFFFFFFF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 0x7
+    recs.append((b, t0, t1, xcc, se, sh, cu, wg))
+t0 = min(r[1] for r in recs)
+t1 = max(r[2] for r in recs)
+print(f"tiles {len(recs)}  span {(t1 - t0) / 100:.2f} us (100 MHz ticks)")
+dur = [(r[2] - r[1]) / 100 for r in recs]
+print(f"tile duration us: min {min(dur):.2f} avg {sum(dur)/len(dur):.2f} max {max(dur):.2f}")
+print("first 8 tiles dur:", [round(x, 1) for x in dur[:8]], " last 8:", [round(x, 1) for x in dur[-8:]])
+per_wg = collections.defaultdict(list)
+for r in recs:
+    per_wg[r[7]].append(r)
+ends = sorted(((max(x[2] for x in v) - t0) / 100, k, len(v)) for k, v in per_wg.items())
+print(f"workgroups {len(per_wg)}; latest-finishing (us, wg, ntiles):", [(round(e, 1), k, n) for e, k, n in ends[-6:]])
+for e, k, n in ends[-3:]:
+    v = sorted(per_wg[k], key=lambda x: x[1])
+    print("  wg", k, "tiles:", [(x[0], round((x[1] - t0) / 100, 1), round((x[2] - x[1]) / 100, 1)) for x in v])
+per_cu = collections.defaultdict(set)
+for r in recs:
+    per_cu[(r[3], r[4], r[5], r[6])].add(r[7])
+cnt = collections.Counter(len(v) for v in per_cu.values())
+print("workgroups per CU histogram:", dict(sorted(cnt.items())), "CUs", len(per_cu))

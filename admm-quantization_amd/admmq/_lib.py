@@ -57,6 +57,7 @@ def load() -> ctypes.CDLL:
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
+        "admmq_debug_set_legacy_stage1": (I32, [I32]),
         "admmq_profile_begin": (I32, [I32]),
         "admmq_profile_end": (I32, [P, P]),
         "admmq_version": (I32, []),
@@ -122,4 +123,24 @@ class exhaustive_search:
 
     def __exit__(self, *exc):
         load().admmq_set_exhaustive_search(0)
+        return False
+
+
+class stage1_form:
+    """Context manager: run stage 1 of the two-stage search in its per-level form
+    (``"legacy"``, k_mse_hist) or its merged-threshold form (``"merged"``,
+    k_mse_prep2 + k_mse_hist2). Both produce the same integers; used as a
+    cross-check in the parity tests. Restores the per-level default on exit."""
+
+    def __init__(self, form: str):
+        if form not in ("legacy", "merged"):
+            raise ValueError(form)
+        self.form = form
+
+    def __enter__(self):
+        load().admmq_debug_set_legacy_stage1(1 if self.form == "legacy" else 0)
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_legacy_stage1(1)
         return False

@@ -23,6 +23,7 @@ constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaus
 constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
 constexpr int kMaxStage1Bits = 6;  // bits handled by the two-stage search (threshold table in LDS)
 constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms (atomic spread)
+constexpr int kMaxMerged = 4096;   // qmax * ncand of the merged-threshold stage 1
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
@@ -41,6 +42,8 @@ struct MseView {
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
   unsigned* ticket;            // [slot] stage-1 blocks finished (the last one runs the selection)
+  float* tsort;                // [kMaxMerged] merged sorted level thresholds (current iteration)
+  unsigned short* tpos;        // [kMaxMerged] L(k, c) = position of thr[k][c] in tsort (1-based count)
   const int* done;             // early-exit flag (ADMM) or nullptr
   int nhist, pad_;             // stage-1 blocks of this job
 };
@@ -105,6 +108,11 @@ size_t hist_lds_bytes(int ncand, int bits);
 int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
+int copy_prep_trace(unsigned long long* host, int n);
+bool merged_ok(int ncand, int bits);
+void launch_mse_prep2(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s);
+void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                      int slot, hipStream_t s);
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);
@@ -117,7 +125,7 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
                    hipStream_t s);
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
-constexpr int kHistElems = 4096;    // elements per stage-1 work unit (1024 threads x float4)
+constexpr int kHistElems = 8192;    // elements per stage-1 work unit (1024 threads x 2 float4)
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 
 }  // namespace admmq

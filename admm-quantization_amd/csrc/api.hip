@@ -52,6 +52,9 @@ struct Prof {
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
+// Stage-1 form: per-level (k_mse_hist, default) or merged thresholds (k_mse_prep2 +
+// k_mse_hist2, ADMMQ_STAGE1=merged). Both give the same integers.
+static bool g_legacy_stage1 = !(getenv("ADMMQ_STAGE1") && std::string(getenv("ADMMQ_STAGE1")) == "merged");
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
@@ -89,6 +92,8 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
   v.ticket = cv.take<unsigned>((size_t)nslot);
+  v.tsort = cv.take<float>((size_t)kMaxMerged);
+  v.tpos = cv.take<unsigned short>((size_t)kMaxMerged);
 }
 
 struct AdmmPlan {
@@ -283,7 +288,12 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
   if (qscheme == kMse) {
     const bool all = exhaustive || !two_stage_ok(ncand, bits);
-    if (!all) launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    if (!all && merged_ok(ncand, bits) && !g_legacy_stage1) {
+      launch_mse_prep2(nullptr, pl.d_jobs, n, ncand, bits, 0, s);
+      launch_mse_hist2(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    } else if (!all) {
+      launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    }
     else launch_mse_select_all(nullptr, pl.d_jobs, n, ncand, 0, s);
     launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
   }
@@ -304,6 +314,12 @@ int32_t admmq_version(void) { return 100; }
 
 int32_t admmq_set_exhaustive_search(int32_t enable) {
   g_exhaustive = enable != 0;
+  return ADMMQ_OK;
+}
+
+// diagnostics (not in include/admmq.h): 1 = per-level stage 1, 0 = merged thresholds
+int32_t admmq_debug_set_legacy_stage1(int32_t enable) {
+  g_legacy_stage1 = enable != 0;
   return ADMMQ_OK;
 }
 
@@ -378,6 +394,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
+  const bool merged = merged_ok(num_attempts, bits) && !g_legacy_stage1;
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);
@@ -385,7 +402,12 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
-      if (!exhaustive) launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      if (!exhaustive && merged) {
+        launch_mse_prep2(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, s);
+        launch_mse_hist2(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      } else if (!exhaustive) {
+        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      }
       else launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
       launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       prof_mark(s);
@@ -402,6 +424,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 // diagnostics (not in include/admmq.h): per-workgroup timeline of the last GEMM launch
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
+int32_t admmq_debug_prep_trace(unsigned long long* host, int32_t n) { return copy_prep_trace(host, n); }
 
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
                                      int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,

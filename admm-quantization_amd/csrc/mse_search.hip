@@ -211,9 +211,13 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   __shared__ int last;
   // this thread's 4 elements: issued first, so the load overlaps the table setup
   const long long total = (long long)v.rows * v.ld;
-  const long long e = (long long)ck.start + 4LL * threadIdx.x;
-  float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < total) x4 = *reinterpret_cast<const float4*>(v.X + e);
+  float4 x4v[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 4096 hh
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * hh;
+    x4v[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x4v[hh] = *reinterpret_cast<const float4*>(v.X + e);
+  }
   fill_thresholds(thr, mx, n, QMAX);
   if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
   for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
@@ -230,10 +234,11 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   double s2 = 0.0;
   unsigned long long full1 = 0ull;
   unsigned full2 = 0u;
-  const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float x = xs[j];
+#pragma unroll 1
+  for (int jj = 0; jj < 8; ++jj) {
+    const float4 q4 = x4v[jj >> 2];
+    const int j4 = jj & 3;
+    const float x = j4 == 0 ? q4.x : (j4 == 1 ? q4.y : (j4 == 2 ? q4.z : q4.w));
     s2 += (double)x * (double)x;
     const float a = __builtin_fabsf(x);
     const int cap = (x > 0.f) ? QMAX - 1 : QMAX;
@@ -352,6 +357,316 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   trace(__builtin_amdgcn_s_memrealtime());
 }
 
+// ---------------------------------------------------------------------------
+// Stage 1, merged-threshold form (qmax * ncand <= kMaxMerged).
+//
+// With B(a) = #{(k, c) : thr[k][c] <= a} over ALL levels and candidates and
+// L(k, c) = #{(k', c') : thr[k'][c'] <= thr[k][c]} (ties counted), for every a >= 0:
+//     a >= thr[k][c]  <=>  B(a) >= L(k, c).
+// So one binary search per element in the sorted merged table places it in bucket
+// B(|x|), and per candidate
+//     T1(c) = sum_k sum{ af : B >= L(k, c) },   T2(c) = sum_k (2k-1) #{ B >= L(k, c) }
+// over the elements allowed level k (x > 0 reaches at most qmax - 1, so the top level
+// reads the negatives' buckets only). These are the same integers as the per-level
+// breakpoint sums of k_mse_hist (each (element, level) pair contributes af once).
+//
+// k_mse_prep2: per job and iteration, thr[k][c] -> sorted table tsort[M] and the
+// positions tpos[(k-1) n + c] = L(k, c) in [1, M] (one 1024-thread block per job).
+__device__ unsigned long long g_prep_trace[256][5];
+int copy_prep_trace(unsigned long long* host, int n) {
+  n = n < 256 ? n : 256;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prep_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
+
+__global__ __launch_bounds__(1024) void k_mse_prep2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                    int ncand, int bits, int slot) {
+  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
+  const MseView& v = mview(d, qj, blockIdx.x);
+  if (v.done && *v.done) return;
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) return;
+  __shared__ float thr[kMaxMerged];
+  const int n = ncand;
+  const int qmax = 1 << (bits - 1);
+  const int M = qmax * n;
+  fill_thresholds(thr, mx, n, qmax);
+  __syncthreads();
+  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
+  // Rank by counting (rows thr[j][.] are non-decreasing): with the total order
+  // (value, level, candidate), thr[k][c] has rank
+  //     sum_{j<k} #{c' : thr[j][c'] <= T} + c + sum_{j>k} #{c' : thr[j][c'] < T}
+  // and L(k, c) = sum_j #{c' : thr[j][c'] <= T}. Row counts start from the linear
+  // estimate t_c ~ S0 + c step (thr[j][c] ~ (2j-1) t_c / den) and walk to the exact one.
+  const float S0 = (float)(0.2 * (double)mx);
+  const float E0 = (float)(1.2 * (double)mx);
+  const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
+  const float den = (float)(2 * qmax - 1);
+  for (int e = threadIdx.x; e < M; e += blockDim.x) {
+    const int k = e / n, c = e - k * n;           // level k+1
+    const float T = thr[e];
+    int rank = c, L = 0;
+    for (int j = 0; j < qmax; ++j) {
+      const float* row = thr + j * n;
+      int le;                                        // #{c' : row[c'] <= T}
+      if (j == k) {
+        le = c + 1;
+        while (le < n && row[le] <= T) ++le;
+      } else {
+        const float tc = T * den / (float)(2 * j + 1);
+        const float ce = (tc - S0) * inv_step;
+        le = (ce < 0.f) ? 0 : (ce >= (float)n ? n : (int)ce + 1);
+        while (le < n && row[le] <= T) ++le;
+        while (le > 0 && row[le - 1] > T) --le;
+      }
+      L += le;
+      if (j < k) rank += le;
+      if (j > k) {
+        int lt = le;                                 // #{c' : row[c'] < T}
+        while (lt > 0 && row[lt - 1] == T) --lt;
+        rank += lt;
+      }
+    }
+    v.tpos[e] = (unsigned short)L;
+    v.tsort[rank] = T;
+  }
+  const unsigned long long T2 = T1;
+  if (threadIdx.x == 0 && blockIdx.x < 256) {
+    g_prep_trace[blockIdx.x][0] = T0; g_prep_trace[blockIdx.x][1] = T1; g_prep_trace[blockIdx.x][2] = T2;
+    g_prep_trace[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime(); g_prep_trace[blockIdx.x][4] = 0;
+  }
+}
+
+// Candidate selection from per-candidate totals T1/T2 (LDS) and S2, by one wave:
+// as select_wave, without the suffix scan.
+__device__ void select_wave2(const MseView& v, int* sel, const unsigned long long* T1v, const unsigned long long* T2v,
+                             double S2, float mx, int n, int qmax) {
+  const int lane = threadIdx.x & 63;
+  const int P = (n + 63) / 64;
+  const int c0 = lane * P, c1 = min(c0 + P, n);
+  SelCtx cx;
+  cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * qmax - 1);
+  cx.u = 0x1p-24;
+  cx.fixu = ldexp(1.0, -hist_fixed_exp(mx, v.nelem, qmax));
+  cx.Kterm = (double)v.nq * ldexp(1.0, -fixed_exp(mx, v.nq));
+  cx.Nterm = (double)((long long)v.nelem * qmax);
+  cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
+  double mymin = 1e300;
+  for (int c = c0; c < c1; ++c) {
+    double lo, hi;
+    cx.bounds(c, T1v[c], T2v[c], lo, hi);
+    mymin = fmin(mymin, hi);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mymin = fmin(mymin, __shfl_xor(mymin, off));
+  unsigned long long keep = 0ull;                  // bit (c - c0) set: c in S (P <= 16)
+  int cnt = 0;
+  for (int c = c0; c < c1; ++c) {
+    double lo, hi;
+    cx.bounds(c, T1v[c], T2v[c], lo, hi);
+    if (lo <= mymin) { keep |= 1ull << (c - c0); ++cnt; }
+  }
+  int pre = cnt;                                   // inclusive prefix over lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(pre, off);
+    if (lane >= off) pre += o;
+  }
+  const int total = __shfl(pre, 63);
+  int pos = pre - cnt;
+  for (int c = c0; c < c1; ++c) {
+    if ((keep >> (c - c0)) & 1ull) {
+      if (pos < kMaxSel) sel[2 + pos] = c;
+      ++pos;
+    }
+  }
+  if (lane == 0) {
+    if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
+    else { sel[0] = total; sel[1] = 0; }
+  }
+}
+
+template <int QMAX>
+__global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                       const Chunk* __restrict__ chunks, int ncand, int slot) {
+  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
+  const Chunk ck = chunks[blockIdx.x];
+  const MseView& v = mview(d, qj, ck.job);
+  if (v.done && *v.done) return;
+  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
+    if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = ncand;
+  const int M = QMAX * n;
+  const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
+  unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
+  unsigned long long* sumN = sumA + nb;
+  unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
+  unsigned* cntN = cntA + nb;
+  float* key = reinterpret_cast<float*>(cntN + nb);                          // M
+  unsigned short* tpos = reinterpret_cast<unsigned short*>(key + M);         // M
+  __shared__ double red[16];
+  __shared__ unsigned long long wtot[16], wtot2[16];
+  __shared__ unsigned wtot32[16], wtot32b[16];
+  __shared__ int last;
+  const long long total = (long long)v.rows * v.ld;
+  float4 x4[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 4096 hh
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * hh;
+    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x4[hh] = *reinterpret_cast<const float4*>(v.X + e);
+  }
+  for (int i = threadIdx.x; i < M; i += blockDim.x) { key[i] = v.tsort[i]; tpos[i] = v.tpos[i]; }
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
+  __syncthreads();
+  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
+  const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
+  const int dummy = M + 1 + (threadIdx.x & 63);
+  const float xs[8] = {x4[0].x, x4[0].y, x4[0].z, x4[0].w, x4[1].x, x4[1].y, x4[1].z, x4[1].w};
+  // binary searches of the 8 elements interleaved (independent LDS chains):
+  // lo = #{thresholds <= |x|}
+  int lo[8], hi[8];
+  float av[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { lo[j] = 0; hi[j] = M; av[j] = __builtin_fabsf(xs[j]); }
+  for (int step = M; step > 0; step >>= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int mid = (lo[j] + hi[j]) >> 1;
+      const bool go = lo[j] < hi[j];
+      const bool le = key[min(mid, M - 1)] <= av[j];
+      lo[j] = (go && le) ? mid + 1 : lo[j];
+      hi[j] = (go && !le) ? mid : hi[j];
+    }
+  }
+  double s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = xs[j];
+    s2 += (double)x * (double)x;
+    const int B = lo[j];                      // 0: reaches no level for any candidate
+    const bool live = B > 0;
+    const int b = live ? B : dummy;
+    const bool neg = x < 0.f;
+    const unsigned long long af = live ? to_fixed(av[j], K1) : 0ull;
+    atomicAdd(neg ? &sumN[b] : &sumA[b], af);
+    atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
+  }
+  __syncthreads();
+  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
+  // all = positives + negatives; then suffix sums S[i] = sum over buckets >= i
+  for (int i = threadIdx.x; i <= M; i += blockDim.x) { sumA[i] += sumN[i]; cntA[i] += cntN[i]; }
+  __syncthreads();
+  {   // suffix sums S[i] = sum_{j >= i} of the four bucket arrays in one block pass:
+      // contiguous per-thread runs, then a scan of the run totals over the 1024 threads
+    const int len = M + 1;
+    const int per = (len + 1023) >> 10;
+    const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
+    unsigned long long r1 = 0ull, r2 = 0ull;
+    unsigned r3 = 0u, r4 = 0u;
+    for (int i = b1 - 1; i >= b0; --i) {
+      r1 += sumA[i]; sumA[i] = r1;
+      r2 += sumN[i]; sumN[i] = r2;
+      r3 += cntA[i]; cntA[i] = r3;
+      r4 += cntN[i]; cntN[i] = r4;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long q1 = r1, q2 = r2;
+    unsigned q3 = r3, q4 = r4;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
+      const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
+      if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
+    }
+    if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
+    __syncthreads();
+    unsigned long long a1 = 0ull, a2 = 0ull;
+    unsigned a3 = 0u, a4 = 0u;
+    for (int j = w + 1; j < 16; ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
+    const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
+    const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
+    if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
+    for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
+    __syncthreads();
+  }
+  // per-candidate totals of this block into one of kHistRep replicas
+  const int rep = blockIdx.x & (kHistRep - 1);
+  unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    unsigned long long t1 = 0ull, t2 = 0ull;
+#pragma unroll
+    for (int k = 1; k < QMAX; ++k) {
+      const int L = tpos[(k - 1) * n + c];
+      t1 += sumA[L];
+      t2 += (unsigned long long)(2 * k - 1) * cntA[L];
+    }
+    const int L = tpos[(QMAX - 1) * n + c];
+    t1 += sumN[L];
+    t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
+    if (t1) atomicAdd(&g1[c], t1);
+    if (t2) atomicAdd(&g2[c], t2);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    atomicAdd(&v.s2[slot], t);
+  }
+  // ticket: the last block of this job selects the candidate set (all its inputs were
+  // written by device-scope atomics: drain them, no L2 writeback needed)
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = (__hip_atomic_fetch_add(&v.ticket[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(v.nhist - 1)) ? 1 : 0;
+  __syncthreads();
+  const unsigned long long T3 = __builtin_amdgcn_s_memrealtime();
+  auto trace = [&](unsigned long long T4) {
+    if (threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
+      g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = T1; g_hist_trace[blockIdx.x][2] = T2;
+      g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4; g_hist_trace[blockIdx.x][5] = 0;
+    }
+  };
+  if (!last) { trace(T3); return; }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  unsigned long long* T1v = sumA;                 // reuse LDS: n each
+  unsigned long long* T2v = sumN;
+  const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
+  const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    unsigned long long t1 = 0ull, t2 = 0ull;
+#pragma unroll
+    for (int r = 0; r < kHistRep; ++r) {
+      t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    T1v[c] = t1; T2v[c] = t2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    select_wave2(v, sel, T1v, T2v, S2, mx, n, QMAX);
+  }
+  trace(__builtin_amdgcn_s_memrealtime());
+}
+
+size_t hist2_lds_bytes(int ncand, int bits) {
+  const size_t M = (size_t)ncand << (bits - 1);
+  const size_t nb = M + 1 + 64;
+  return nb * (8 + 8 + 4 + 4) + M * 4 + ((M * 2 + 15) & ~(size_t)15);
+}
+
 size_t hist_lds_bytes(int ncand, int bits) {
   const int qmax = 1 << (bits - 1);
   const size_t nb = (size_t)ncand + 1 + 64;
@@ -417,6 +732,24 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
     case 4: hipLaunchKernelGGL(k_mse_hist<8>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
     case 5: hipLaunchKernelGGL(k_mse_hist<16>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
     default: hipLaunchKernelGGL(k_mse_hist<32>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+  }
+}
+bool merged_ok(int ncand, int bits) {
+  return ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist2_lds_bytes(ncand, bits) <= 150 * 1024;
+}
+void launch_mse_prep2(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(k_mse_prep2, dim3(njobs), dim3(1024), 0, s, d, q, ncand, bits, slot);
+}
+void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
+                      int slot, hipStream_t s) {
+  if (nchunks <= 0) return;
+  const size_t lds = hist2_lds_bytes(ncand, bits);
+  switch (bits) {
+    case 1: hipLaunchKernelGGL(k_mse_hist2<1>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
+    case 2: hipLaunchKernelGGL(k_mse_hist2<2>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
+    case 3: hipLaunchKernelGGL(k_mse_hist2<4>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
+    case 4: hipLaunchKernelGGL(k_mse_hist2<8>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
+    default: hipLaunchKernelGGL(k_mse_hist2<16>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
   }
 }
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {

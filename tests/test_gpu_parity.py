@@ -49,11 +49,21 @@ def _rel(a, b):
 
 
 # ----------------------------------------------------------------------------- P1
-def test_quantizer_reference_kats(torch_dev):
+@pytest.mark.parametrize("stage1", ["legacy", "merged"])
+def test_quantizer_reference_kats(torch_dev, stage1):
+    """Every committed reference KAT, bit-exact, with either stage-1 form."""
     torch, dev = torch_dev
     from admmq import quantize_tensor
+    from admmq._lib import stage1_form
     with open(os.path.join(GOLDEN, "f1_quant.json")) as f:
         meta = json.load(f)
+    bad = []
+    with stage1_form(stage1):
+        bad = _run_kats(torch, dev, quantize_tensor, meta)
+    assert bad == [], f"{len(bad)} reference KATs differ on the GPU: {bad[:20]}"
+
+
+def _run_kats(torch, dev, quantize_tensor, meta):
     bad = []
     for case in meta:
         x = gc.f1_input(case)
@@ -66,7 +76,7 @@ def test_quantizer_reference_kats(torch_dev):
         assert y.shape == x.shape
         if gc.canonical_sha(y) != case["sha"]:
             bad.append(case["id"])
-    assert bad == [], f"{len(bad)} reference KATs differ on the GPU: {bad[:20]}"
+    return bad
 
 
 @pytest.mark.parametrize("shape,bits,na", [((9, 134), 4, 200), ((64, 134), 2, 200), ((512, 1141), 4, 200),
@@ -81,12 +91,14 @@ def test_sse_table_matches_oracle(torch_dev, shape, bits, na):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("stage1", ["merged", "legacy"])
 @pytest.mark.parametrize("seed", range(6))
-def test_two_stage_search_equals_exhaustive(torch_dev, seed):
-    """The default two-stage search returns exactly the exhaustive sweep's answer."""
+def test_two_stage_search_equals_exhaustive(torch_dev, seed, stage1):
+    """The default two-stage search (either stage-1 form) returns exactly the
+    exhaustive sweep's answer."""
     torch, dev = torch_dev
     from admmq import quantize_batched
-    from admmq._lib import exhaustive_search
+    from admmq._lib import exhaustive_search, stage1_form
     rng = np.random.default_rng(100 + seed)
     shapes = [(9, 134), (512, 1141), (64, 278), (3, 5), (128, 759), (1, 1)]
     xs = []
@@ -95,18 +107,20 @@ def test_two_stage_search_equals_exhaustive(torch_dev, seed):
         if seed % 2:
             x.flat[rng.integers(x.size)] *= 30.0
         xs.append(_t(torch, dev, x.astype(np.float32)))
-    for bits in (2, 4, 8):
-        fast = quantize_batched(xs, bits, MSE)
+    for bits in (2, 3, 4, 5, 6, 8):
+        with stage1_form(stage1):
+            fast = quantize_batched(xs, bits, MSE)
         with exhaustive_search():
             slow = quantize_batched(xs, bits, MSE)
         for f, s_ in zip(fast, slow):
             assert _bits_equal(f.cpu().numpy(), s_.cpu().numpy())
 
 
-def test_two_stage_admm_equals_exhaustive(torch_dev):
+@pytest.mark.parametrize("stage1", ["merged", "legacy"])
+def test_two_stage_admm_equals_exhaustive(torch_dev, stage1):
     torch, dev = torch_dev
     from admmq import admm_iteration_batched
-    from admmq._lib import exhaustive_search
+    from admmq._lib import exhaustive_search, stage1_form
     probs_np = [_layer_problem(l, m) for l, m in [("layer1.0.conv1", 0), ("layer3.1.conv2", 1), ("layer4.1.conv1", 2)]]
 
     def run():
@@ -115,7 +129,8 @@ def test_two_stage_admm_equals_exhaustive(torch_dev):
         Hs = admm_iteration_batched(ps, 8, 0.0, 4, MSE)
         return [(h.cpu().numpy(), p[1].cpu().numpy()) for h, p in zip(Hs, ps)]
 
-    fast = run()
+    with stage1_form(stage1):
+        fast = run()
     with exhaustive_search():
         slow = run()
     for f, s_ in zip(fast, slow):

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_rho(const ProbDesc* __restrict__ probs)
     for (int sl = 0; sl < 2; ++sl) {
       unsigned* st = p.mv.stat + 4 * sl;
       st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
-      for (int k = 0; k < 4; ++k) p.res[4 * sl + k] = 0.0;
+      for (int k = 0; k < 4 * kResRep; ++k) p.res[4 * kResRep * sl + k] = 0.0;
     }
   }
 }
@@ -65,27 +65,41 @@ __global__ __launch_bounds__(256) void k_fill_a64(const ProbDesc* __restrict__ p
   }
 }
 
+template <int G>   // float4 groups per thread: 256 G * 4 elements per work unit
 __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restrict__ probs, const Chunk* __restrict__ chunks,
                                                        int ncand, int bits, int scheme, int slot, int iter) {
   const Chunk ck = chunks[blockIdx.x];
   const ProbDesc& p = probs[ck.job];
   if (p.flags[0]) return;
+  const long long total = (long long)p.I * p.ld;
+  // float4 group g of thread t at start + 4 t + 1024 g. Element loads first: independent
+  // of the quantizer parameters, so their latency overlaps the parameter chain
+  // (stat -> sel -> sse) below.
+  float4 x4[G], t4[G], h4[G], u4[G], f4[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
+    x4[g] = make_float4(0.f, 0.f, 0.f, 0.f); t4[g] = x4[g]; h4[g] = x4[g]; u4[g] = x4[g]; f4[g] = x4[g];
+    if (e < total) {
+      x4[g] = *reinterpret_cast<const float4*>(p.X + e);
+      t4[g] = *reinterpret_cast<const float4*>(p.HT + e);
+      h4[g] = *reinterpret_cast<const float4*>(p.H + e);
+      u4[g] = *reinterpret_cast<const float4*>(p.U + e);
+      f4[g] = *reinterpret_cast<const float4*>(p.Fp + e);
+    }
+  }
   const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);
   const float rho = p.rho[0];
-  const long long total = (long long)p.I * p.ld;
-  const long long e = (long long)ck.start + 4LL * threadIdx.x;
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
-  if (e < total) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
+    if (e >= total) continue;
     const int row = (int)(e / p.ld);
     const int c0 = (int)(e - (long long)row * p.ld);
-    const float4 x4 = *reinterpret_cast<const float4*>(p.X + e);
-    const float4 t4 = *reinterpret_cast<const float4*>(p.HT + e);
-    const float4 h4 = *reinterpret_cast<const float4*>(p.H + e);
-    const float4 u4 = *reinterpret_cast<const float4*>(p.U + e);
-    const float4 f4 = *reinterpret_cast<const float4*>(p.Fp + e);
-    const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, ts[4] = {t4.x, t4.y, t4.z, t4.w};
-    const float hs[4] = {h4.x, h4.y, h4.z, h4.w}, us[4] = {u4.x, u4.y, u4.z, u4.w};
-    const float fs[4] = {f4.x, f4.y, f4.z, f4.w};
+    const float xs[4] = {x4[g].x, x4[g].y, x4[g].z, x4[g].w}, ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
+    const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
+    const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
     float ho[4], uo[4], po[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -118,14 +132,14 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
   if (threadIdx.x < 4) {
     double v = 0.0;
     for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[k][threadIdx.x];
-    atomicAdd(&p.res[4 * slot + threadIdx.x], v);
+    atomicAdd(&p.res[4 * (kResRep * slot + (blockIdx.x & (kResRep - 1))) + threadIdx.x], v);
   }
   if (ck.start == 0 && threadIdx.x == 0) {
     p.flags[1] = iter + 1;
     unsigned* st = p.mv.stat + 4 * (slot ^ 1);
     st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
-    double* rs = p.res + 4 * (slot ^ 1);
-    rs[0] = 0.0; rs[1] = 0.0; rs[2] = 0.0; rs[3] = 0.0;
+    double* rs = p.res + 4 * kResRep * (slot ^ 1);
+    for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
   }
 }
 
@@ -155,10 +169,13 @@ void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s) {
   const int nb = (int)std::min<long long>(1024, (tot + 255) / 256);
   hipLaunchKernelGGL(k_fill_a64, dim3(nb, nprob), dim3(256), 0, s, d);
 }
-void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
-                          int slot, int iter, hipStream_t s) {
-  if (nchunks > 0)
-    hipLaunchKernelGGL(k_finalize_admm, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int chunk_elems, int ncand, int bits,
+                          int qscheme, int slot, int iter, hipStream_t s) {
+  if (nchunks <= 0) return;
+  if (chunk_elems == 4096)
+    hipLaunchKernelGGL(k_finalize_admm<4>, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
+  else
+    hipLaunchKernelGGL(k_finalize_admm<1>, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
 }
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s) {
   const long long tot = (long long)maxI * maxR;

@@ -8,7 +8,8 @@
 //                        symmetric, zero outside the R x R block
 //   A64, L64           : float64 [ldm x ldm] SPD factor / inverse-factor scratch
 //   D64                : float64 [ldm x 32] diagonal Cholesky blocks
-//   res[2][4]          : per parity slot, fp64 residual sums S1..S4 (source/admm.py:62-63)
+//   res[2][kResRep][4] : per parity slot, kResRep replicas of the fp64 residual sums
+//                        S1..S4 (source/admm.py:62-63), summed by the convergence test
 //   flags[4]           : {done, iterations, spd_error, 0}
 // and one MseView of per-slot quantizer state (below).
 #pragma once
@@ -23,7 +24,8 @@ constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaus
 constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
 constexpr int kMaxStage1Bits = 6;  // bits handled by the two-stage search (threshold table in LDS)
 constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms (atomic spread)
-constexpr int kMaxMerged = 4096;   // qmax * ncand of the merged-threshold stage 1
+constexpr int kMaxMerged = 4096;
+constexpr int kResRep = 8;         // replicas of the per-problem residual sums (atomic spread)   // qmax * ncand of the merged-threshold stage 1
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
@@ -109,6 +111,7 @@ int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_prep_trace(unsigned long long* host, int n);
+int copy_sel_stats(unsigned long long* host, int reset);
 bool merged_ok(int ncand, int bits);
 void launch_mse_prep2(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s);
 void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
@@ -116,7 +119,7 @@ void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);
-void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int ncand, int bits,
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int chunk_elems, int ncand, int bits,
                           int qscheme, int slot, int iter, hipStream_t s);
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
 
@@ -125,7 +128,9 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
                    hipStream_t s);
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
-constexpr int kHistElems = 8192;    // elements per stage-1 work unit (1024 threads x 2 float4)
+constexpr int kHistElems = 4096;    // elements per stage-1 work unit (1024 x 4 legacy, 512 x 8 merged)
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
+constexpr int kFinElems = 4096;     // elements per ADMM finalize work unit when there are >= kFinMinUnits of them
+constexpr int kFinMinUnits = 256;   //   (else kElemChunk: small problem sets keep their parallelism)
 
 }  // namespace admmq

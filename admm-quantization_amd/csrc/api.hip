@@ -109,6 +109,7 @@ struct AdmmPlan {
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
   int ntiles_big = 0, ntiles_small = 0;
+  int fin_elems = kElemChunk;
 };
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
@@ -137,7 +138,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.A64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.L64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.D64 = cv.take<double>((size_t)d.ldm * 32);
-    d.res = cv.take<double>(8);
+    d.res = cv.take<double>(2 * kResRep * 4);
     d.flags = cv.take<int>(4);
     d.rho = cv.take<float>(4);
     carve_view(cv, d.mv, 2, ncand);
@@ -172,11 +173,14 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
   pl.hist_chunks.clear();
+  long long big_units = 0;
+  for (int i = 0; i < nprob; ++i) big_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kFinElems - 1) / kFinElems;
+  pl.fin_elems = big_units >= kFinMinUnits ? kFinElems : kElemChunk;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
     const long long tot = (long long)d.I * d.ld;
-    for (long long e = 0; e < tot; e += kElemChunk) pl.fin_chunks.push_back({i, (int)e});
+    for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
     for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
     pl.desc[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
@@ -293,9 +297,10 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
       launch_mse_hist2(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
     } else if (!all) {
       launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    } else {   // exhaustive: every candidate's canonical SSE over all chunks
+      launch_mse_select_all(nullptr, pl.d_jobs, n, ncand, 0, s);
+      launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
     }
-    else launch_mse_select_all(nullptr, pl.d_jobs, n, ncand, 0, s);
-    launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
   }
   if (final_pass) launch_qfinal(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), ncand, bits, qscheme, s);
   return check_hip("quantize");
@@ -402,18 +407,20 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
+      // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
         launch_mse_prep2(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, s);
         launch_mse_hist2(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
       } else if (!exhaustive) {
         launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+      } else {
+        launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
+        launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       }
-      else launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
-      launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
       prof_mark(s);
     }
     prof_class(2); prof_mark(s);
-    launch_finalize_admm(pl.d_desc, pl.d_fin, nfin, num_attempts, bits, qscheme, slot, it, s);
+    launch_finalize_admm(pl.d_desc, pl.d_fin, nfin, pl.fin_elems, num_attempts, bits, qscheme, slot, it, s);
     prof_mark(s);
   }
   if (max_iter > 1) launch_unpack(pl.d_desc, nprob, pl.maxI, pl.maxR, s);
@@ -425,6 +432,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_prep_trace(unsigned long long* host, int32_t n) { return copy_prep_trace(host, n); }
+int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
                                      int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,

@@ -38,9 +38,12 @@ constexpr int BN = 64, BK = 32;
 
 __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_prev, int iter, float eps) {
   if (iter == 0) return false;
-  const double* r = p.res + 4 * slot_prev;
-  const double rr = r[0] / r[1];
-  const double ss = r[2] / r[3];
+  const double* r = p.res + 4 * kResRep * slot_prev;   // kResRep replicas of {S1, S2, S3, S4}
+  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < kResRep; ++q)
+    for (int k = 0; k < 4; ++k) t[k] += r[4 * q + k];
+  const double rr = t[0] / t[1];
+  const double ss = t[2] / t[3];
   return (rr < (double)eps) && (ss < (double)eps);
 }
 

@@ -68,6 +68,18 @@ int copy_hist_trace(unsigned long long* host, int n) {
              ? n : -1;
 }
 
+// Diagnostics: how often the selection leaves more than one candidate ({|S| == 1,
+// 2..kMaxSel, exhaustive} counts since the last reset), for admmq_debug_sel_stats.
+__device__ unsigned long long g_sel_stats[3];
+int copy_sel_stats(unsigned long long* host, int reset) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sel_stats), sizeof(g_sel_stats)) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[3] = {0ull, 0ull, 0ull};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_stats), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 3;
+}
+
 // Threshold table of one job into LDS: thr[(k-1) n + c] = smallest a with
 // |q_c(a)| >= k, for k = 1..qmax (increasing in c and in k).
 __device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax) {
@@ -111,8 +123,8 @@ struct SelCtx {
   }
 };
 
-__device__ void select_wave(const MseView& v, int* sel, const unsigned long long* H1, const unsigned long long* H2,
-                            double S2, float mx, int n, int qmax) {
+__device__ void select_wave(const MseView& v, int* sel, int* lsel, const unsigned long long* H1,
+                            const unsigned long long* H2, double S2, float mx, int n, int qmax) {
   const int lane = threadIdx.x & 63;
   const int P = (n + 63) / 64;
   const int c0 = lane * P, c1 = min(c0 + P, n);   // this lane's candidates [c0, c1)
@@ -168,13 +180,39 @@ __device__ void select_wave(const MseView& v, int* sel, const unsigned long long
   int pos = pre - cnt;
   for (int c = c0; c < c1; ++c) {
     if ((keep >> (c - c0)) & 1ull) {
-      if (pos < kMaxSel) sel[2 + pos] = c;
+      if (pos < kMaxSel) { sel[2 + pos] = c; lsel[2 + pos] = c; }
       ++pos;
     }
   }
   if (lane == 0) {   // sel = {|S| (n: exhaustive), unused, S ascending...}; |S| == 1 -> c* = sel[2]
     if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
     else { sel[0] = total; sel[1] = 0; }
+    lsel[0] = sel[0]; lsel[1] = sel[1];
+    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+  }
+}
+
+// Stage 2 inside the last stage-1 block of a job (|S| > 1 is rare: ~0.1 % of the
+// selections on the benchmark workload): the canonical SSE of every candidate in S
+// (or of all of them) over the job's quads, 512-quad tiles staged in LDS, into v.sse.
+// Removes a separate stage-2 launch from every iteration.
+__device__ void sse_in_block(const MseView& v, const int* lsel, int ncand, int bits, int slot, float mx, float4* xs) {
+  const int ns = lsel[0];
+  if (ns == 1) return;
+  const bool all = ns >= ncand;
+  const int K = fixed_exp(mx, v.nq);
+  for (int q0 = 0; q0 < v.nq; q0 += kSseQuads) {
+    const int nqc = min(kSseQuads, v.nq - q0);
+    for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
+      const int qi = q0 + t;
+      const int row = qi / v.qpr;
+      const int qc = qi - row * v.qpr;
+      xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+    }
+    __syncthreads();
+    sse_sweep_list(xs, nqc, mx, K, ncand, bits, all ? nullptr : lsel + 2, all ? ncand : ns,
+                   v.sse + (size_t)slot * ncand);
+    __syncthreads();
   }
 }
 
@@ -211,13 +249,9 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   __shared__ int last;
   // this thread's 4 elements: issued first, so the load overlaps the table setup
   const long long total = (long long)v.rows * v.ld;
-  float4 x4v[2];
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 4096 hh
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * hh;
-    x4v[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4v[hh] = *reinterpret_cast<const float4*>(v.X + e);
-  }
+  const long long e = (long long)ck.start + 4LL * threadIdx.x;
+  float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total) x4 = *reinterpret_cast<const float4*>(v.X + e);
   fill_thresholds(thr, mx, n, QMAX);
   if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
   for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
@@ -234,11 +268,10 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   double s2 = 0.0;
   unsigned long long full1 = 0ull;
   unsigned full2 = 0u;
-#pragma unroll 1
-  for (int jj = 0; jj < 8; ++jj) {
-    const float4 q4 = x4v[jj >> 2];
-    const int j4 = jj & 3;
-    const float x = j4 == 0 ? q4.x : (j4 == 1 ? q4.y : (j4 == 2 ? q4.z : q4.w));
+  const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = xs[j];
     s2 += (double)x * (double)x;
     const float a = __builtin_fabsf(x);
     const int cap = (x > 0.f) ? QMAX - 1 : QMAX;
@@ -344,16 +377,14 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
     H1[b] = t1; H2[b] = t2;
   }
   __syncthreads();
-  if ((abl & 16) && threadIdx.x < 64) {   // timing ablation: the selection twice (same result)
-    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    select_wave(v, sel, H1, H2, S2, mx, n, QMAX);
-  }
+  __shared__ int lsel[2 + kMaxSel];
   if (threadIdx.x < 64) {
     const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
-    select_wave(v, sel, H1, H2, S2, mx, n, QMAX);
+    select_wave(v, sel, lsel, H1, H2, S2, mx, n, QMAX);
   }
+  __syncthreads();
+  sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
   trace(__builtin_amdgcn_s_memrealtime());
 }
 
@@ -439,8 +470,8 @@ __global__ __launch_bounds__(1024) void k_mse_prep2(const ProbDesc* __restrict__
 
 // Candidate selection from per-candidate totals T1/T2 (LDS) and S2, by one wave:
 // as select_wave, without the suffix scan.
-__device__ void select_wave2(const MseView& v, int* sel, const unsigned long long* T1v, const unsigned long long* T2v,
-                             double S2, float mx, int n, int qmax) {
+__device__ void select_wave2(const MseView& v, int* sel, int* lsel, const unsigned long long* T1v,
+                             const unsigned long long* T2v, double S2, float mx, int n, int qmax) {
   const int lane = threadIdx.x & 63;
   const int P = (n + 63) / 64;
   const int c0 = lane * P, c1 = min(c0 + P, n);
@@ -476,18 +507,20 @@ __device__ void select_wave2(const MseView& v, int* sel, const unsigned long lon
   int pos = pre - cnt;
   for (int c = c0; c < c1; ++c) {
     if ((keep >> (c - c0)) & 1ull) {
-      if (pos < kMaxSel) sel[2 + pos] = c;
+      if (pos < kMaxSel) { sel[2 + pos] = c; lsel[2 + pos] = c; }
       ++pos;
     }
   }
   if (lane == 0) {
     if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
     else { sel[0] = total; sel[1] = 0; }
+    lsel[0] = sel[0]; lsel[1] = sel[1];
+    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
   }
 }
 
 template <int QMAX>
-__global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+__global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
                                                        const Chunk* __restrict__ chunks, int ncand, int slot) {
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   const Chunk ck = chunks[blockIdx.x];
@@ -516,8 +549,8 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restric
   const long long total = (long long)v.rows * v.ld;
   float4 x4[2];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 4096 hh
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * hh;
+  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 2048 hh
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
     x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < total) x4[hh] = *reinterpret_cast<const float4*>(v.X + e);
   }
@@ -565,7 +598,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restric
   {   // suffix sums S[i] = sum_{j >= i} of the four bucket arrays in one block pass:
       // contiguous per-thread runs, then a scan of the run totals over the 1024 threads
     const int len = M + 1;
-    const int per = (len + 1023) >> 10;
+    const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
     const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
     unsigned long long r1 = 0ull, r2 = 0ull;
     unsigned r3 = 0u, r4 = 0u;
@@ -588,7 +621,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restric
     __syncthreads();
     unsigned long long a1 = 0ull, a2 = 0ull;
     unsigned a3 = 0u, a4 = 0u;
-    for (int j = w + 1; j < 16; ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
+    for (int j = w + 1; j < (int)(blockDim.x >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
     const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
     const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
     if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
@@ -619,7 +652,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restric
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
-    for (int w = 0; w < 16; ++w) t += red[w];
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
     atomicAdd(&v.s2[slot], t);
   }
   // ticket: the last block of this job selects the candidate set (all its inputs were
@@ -653,25 +686,28 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist2(const ProbDesc* __restric
     T1v[c] = t1; T2v[c] = t2;
   }
   __syncthreads();
+  __shared__ int lsel[2 + kMaxSel];
   if (threadIdx.x < 64) {
     const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
-    select_wave2(v, sel, T1v, T2v, S2, mx, n, QMAX);
+    select_wave2(v, sel, lsel, T1v, T2v, S2, mx, n, QMAX);
   }
+  __syncthreads();
+  sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
   trace(__builtin_amdgcn_s_memrealtime());
 }
 
 size_t hist2_lds_bytes(int ncand, int bits) {
   const size_t M = (size_t)ncand << (bits - 1);
   const size_t nb = M + 1 + 64;
-  return nb * (8 + 8 + 4 + 4) + M * 4 + ((M * 2 + 15) & ~(size_t)15);
+  return std::max(nb * (8 + 8 + 4 + 4) + M * 4 + ((M * 2 + 15) & ~(size_t)15), (size_t)kSseQuads * 16);
 }
 
 size_t hist_lds_bytes(int ncand, int bits) {
   const int qmax = 1 << (bits - 1);
   const size_t nb = (size_t)ncand + 1 + 64;
   const size_t thr = std::max((size_t)qmax * ncand * 4, (size_t)(ncand + 1) * 8);   // also holds H2 sums
-  return nb * 8 + ((nb + 3) & ~(size_t)3) * 4 + thr;
+  return std::max(nb * 8 + ((nb + 3) & ~(size_t)3) * 4 + thr, (size_t)kSseQuads * 16);   // >= stage-2 tile
 }
 
 // Exhaustive / degenerate path only (stage 1 not run): sel = {n, -1} or {1, 0}.
@@ -694,29 +730,44 @@ __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d,
                                                  int slot) {
   __shared__ float4 xs[kSseQuads];
   __shared__ int list[kMaxSel];
-  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-    const Chunk ck = chunks[ci];
-    const MseView& v = mview(d, qj, ck.job);
-    if (v.done && *v.done) continue;
-    const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-    const int ns = sel[0];
-    if (ns == 1) continue;
-    const float mx = __uint_as_float(v.stat[4 * slot]);
-    if (mse_degenerate(mx)) continue;
-    const int nqc = min(kSseQuads, v.nq - ck.start);
-    __syncthreads();   // previous chunk's LDS reads are done
-    for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
-      const int qi = ck.start + t;
-      const int row = qi / v.qpr;
-      const int qc = qi - row * v.qpr;
-      xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+  __shared__ int todo[256];
+  __shared__ int ntodo;
+  // one pass of parallel checks (chunk -> job -> done / |S|): almost always nothing to do
+  if (threadIdx.x == 0) ntodo = 0;
+  __syncthreads();
+  for (int base = blockIdx.x; base < nchunks; base += gridDim.x * (int)blockDim.x) {
+    const int ci = base + threadIdx.x * gridDim.x;
+    if (ci < nchunks) {
+      const Chunk ck = chunks[ci];
+      const MseView& v = mview(d, qj, ck.job);
+      const bool live = !(v.done && *v.done) && v.sel[(size_t)slot * (2 + kMaxSel)] != 1 &&
+                        !mse_degenerate(__uint_as_float(v.stat[4 * slot]));
+      if (live) todo[atomicAdd(&ntodo, 1)] = ci;
     }
-    const bool all = ns >= ncand;
-    if (!all)
-      for (int j = threadIdx.x; j < ns; j += blockDim.x) list[j] = sel[2 + j];
     __syncthreads();
-    sse_sweep_list(xs, nqc, mx, fixed_exp(mx, v.nq), ncand, bits, all ? nullptr : list, all ? ncand : ns,
-                   v.sse + (size_t)slot * ncand);
+    for (int w = 0; w < ntodo; ++w) {
+      const Chunk ck = chunks[todo[w]];
+      const MseView& v = mview(d, qj, ck.job);
+      const int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+      const int ns = sel[0];
+      const float mx = __uint_as_float(v.stat[4 * slot]);
+      const int nqc = min(kSseQuads, v.nq - ck.start);
+      for (int t = threadIdx.x; t < nqc; t += blockDim.x) {
+        const int qi = ck.start + t;
+        const int row = qi / v.qpr;
+        const int qc = qi - row * v.qpr;
+        xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+      }
+      const bool all = ns >= ncand;
+      if (!all)
+        for (int j = threadIdx.x; j < ns; j += blockDim.x) list[j] = sel[2 + j];
+      __syncthreads();
+      sse_sweep_list(xs, nqc, mx, fixed_exp(mx, v.nq), ncand, bits, all ? nullptr : list, all ? ncand : ns,
+                     v.sse + (size_t)slot * ncand);
+      __syncthreads();   // xs / list reused by the next chunk
+    }
+    if (threadIdx.x == 0) ntodo = 0;
+    __syncthreads();
   }
 }
 
@@ -745,11 +796,11 @@ void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
   if (nchunks <= 0) return;
   const size_t lds = hist2_lds_bytes(ncand, bits);
   switch (bits) {
-    case 1: hipLaunchKernelGGL(k_mse_hist2<1>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
-    case 2: hipLaunchKernelGGL(k_mse_hist2<2>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
-    case 3: hipLaunchKernelGGL(k_mse_hist2<4>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
-    case 4: hipLaunchKernelGGL(k_mse_hist2<8>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
-    default: hipLaunchKernelGGL(k_mse_hist2<16>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot); break;
+    case 1: hipLaunchKernelGGL(k_mse_hist2<1>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
+    case 2: hipLaunchKernelGGL(k_mse_hist2<2>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
+    case 3: hipLaunchKernelGGL(k_mse_hist2<4>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
+    case 4: hipLaunchKernelGGL(k_mse_hist2<8>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
+    default: hipLaunchKernelGGL(k_mse_hist2<16>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
   }
 }
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {
@@ -758,8 +809,8 @@ void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncan
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s) {
   if (nchunks > 0)
-    hipLaunchKernelGGL(k_mse_sse, dim3(std::min(nchunks, 512)), dim3(256), 0, s, d, q, chunks, nchunks, ncand, bits,
-                       slot);
+    hipLaunchKernelGGL(k_mse_sse, dim3(std::min((nchunks + 255) / 256 * 4, 1024)), dim3(256), 0, s, d, q, chunks, nchunks,
+                       ncand, bits, slot);
 }
 
 }  // namespace admmq

@@ -95,6 +95,17 @@ def gather_factors(runs, rank, world, device):
     return sum(int(s.item()) for s in sizes)
 
 
+def reduce_over_ranks(elapsed, factor_iters, world, device):
+    """Whole-job rate inputs: the slowest rank's elapsed time (MAX) and the
+    factor-iterations all ranks processed (SUM)."""
+    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    fi = torch.tensor([float(factor_iters)], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fi, op=dist.ReduceOp.SUM)
+    return float(el.item()), float(fi.item())
+
+
 def algorithmic_flops(work, max_iter_admm, num_attempts=200):
     """Per step: SSE sweep 8 flops x candidates x elements (SURVEY §8(d) F_valu) and the
     solve GEMM 2 I R^2, summed over (layer, mode) x inner iterations."""
@@ -214,13 +225,7 @@ def main():
         _lib.check(lib.admmq_profile_end(ms, cnt), "profile_end")
         kern = {"ms": list(ms), "launches": list(cnt)}
 
-    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    fi = torch.tensor([fi_per_step * a.steps], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(fi, op=dist.ReduceOp.SUM)
-    elapsed_max = float(el.item())
-    total_fi = float(fi.item())
+    elapsed_max, total_fi = reduce_over_ranks(elapsed, fi_per_step * a.steps, world, device)
 
     if rank == 0:
         out = {"metric": METRIC, "value": total_fi / elapsed_max, "unit": "factor-iterations/s", "n_gpus": world,

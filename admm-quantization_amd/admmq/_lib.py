@@ -130,7 +130,7 @@ class stage1_form:
     """Context manager: run stage 1 of the two-stage search in its per-level form
     (``"legacy"``, k_mse_hist) or its merged-threshold form (``"merged"``,
     k_mse_prep2 + k_mse_hist2). Both produce the same integers; used as a
-    cross-check in the parity tests. Restores the per-level default on exit."""
+    cross-check in the parity tests. Restores the merged default on exit."""
 
     def __init__(self, form: str):
         if form not in ("legacy", "merged"):
@@ -142,5 +142,5 @@ class stage1_form:
         return self
 
     def __exit__(self, *exc):
-        load().admmq_debug_set_legacy_stage1(1)
+        load().admmq_debug_set_legacy_stage1(0)
         return False

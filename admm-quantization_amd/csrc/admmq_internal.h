@@ -44,8 +44,6 @@ struct MseView {
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
   unsigned* ticket;            // [slot] stage-1 blocks finished (the last one runs the selection)
-  float* tsort;                // [kMaxMerged] merged sorted level thresholds (current iteration)
-  unsigned short* tpos;        // [kMaxMerged] L(k, c) = position of thr[k][c] in tsort (1-based count)
   const int* done;             // early-exit flag (ADMM) or nullptr
   int nhist, pad_;             // stage-1 blocks of this job
 };
@@ -105,17 +103,16 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
                  int slot, int iter, float eps, int ncand, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
-                     int slot, hipStream_t s);
+                     int slot, int nv, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
 int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
-int copy_prep_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
+int check_thresholds(unsigned seed, int nsamp);
 bool merged_ok(int ncand, int bits);
-void launch_mse_prep2(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s);
-void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
-                      int slot, hipStream_t s);
+void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
+                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s);
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);
@@ -128,7 +125,8 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
                    hipStream_t s);
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
-constexpr int kHistElems = 4096;    // elements per stage-1 work unit (1024 x 4 legacy, 512 x 8 merged)
+constexpr int kHistElems = 4096;    // elements per stage-1 work unit x hist_nv (1024 x 4 legacy, 512 x 8 merged)
+constexpr int kHistMaxUnits = 512;  // stage-1 units that fit in one round (2 per CU): above, 2x larger units
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 constexpr int kFinElems = 4096;     // elements per ADMM finalize work unit when there are >= kFinMinUnits of them
 constexpr int kFinMinUnits = 256;   //   (else kElemChunk: small problem sets keep their parallelism)

@@ -52,13 +52,42 @@ struct Prof {
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
-// Stage-1 form: per-level (k_mse_hist, default) or merged thresholds (k_mse_prep2 +
-// k_mse_hist2, ADMMQ_STAGE1=merged). Both give the same integers.
-static bool g_legacy_stage1 = !(getenv("ADMMQ_STAGE1") && std::string(getenv("ADMMQ_STAGE1")) == "merged");
+// Stage-1 form: merged thresholds (k_mse_hist3, default where supported) or per-level
+// (k_mse_hist; ADMMQ_STAGE1=legacy, and wherever merged_tables/merged_ok decline). Both
+// give the same integers.
+static bool g_legacy_stage1 = getenv("ADMMQ_STAGE1") && std::string(getenv("ADMMQ_STAGE1")) == "legacy";
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
   return !g_exhaustive && ncand <= kMaxStage1 && bits <= kMaxStage1Bits && hist_lds_bytes(ncand, bits) <= 64 * 1024;
+}
+
+// Exact merged order of the level thresholds for (n, qmax) (k_mse_hist3): thr[k][c] is
+// within a few ulps of (2k-1) ((n-1) + 5c) times a constant, so the integer keys give
+// the order; rank0[e] for e = (k-1) n + c, and the groups of equal keys as
+// {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
+// than 4 (the per-level stage 1 is used instead).
+static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, std::vector<unsigned short>& groups) {
+  const int M = qmax * n;
+  std::vector<std::pair<long long, int>> key(M);
+  for (int k = 1; k <= qmax; ++k)
+    for (int c = 0; c < n; ++c) key[(k - 1) * n + c] = {(long long)(2 * k - 1) * ((n - 1) + 5LL * c), (k - 1) * n + c};
+  std::sort(key.begin(), key.end());
+  rank0.assign(M, 0);
+  groups.clear();
+  for (int r = 0; r < M;) {
+    int r1 = r + 1;
+    while (r1 < M && key[r1].first == key[r].first) ++r1;
+    for (int j = r; j < r1; ++j) rank0[key[j].second] = (unsigned short)j;
+    if (r1 - r > 1) {
+      if (r1 - r > 4) return false;
+      unsigned short g[6] = {(unsigned short)r, (unsigned short)(r1 - r), 0, 0, 0, 0};
+      for (int j = r; j < r1; ++j) g[2 + j - r] = (unsigned short)key[j].second;
+      groups.insert(groups.end(), g, g + 6);
+    }
+    r = r1;
+  }
+  return true;
 }
 
 static inline void prof_mark(hipStream_t s) {
@@ -92,8 +121,7 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
   v.ticket = cv.take<unsigned>((size_t)nslot);
-  v.tsort = cv.take<float>((size_t)kMaxMerged);
-  v.tpos = cv.take<unsigned short>((size_t)kMaxMerged);
+
 }
 
 struct AdmmPlan {
@@ -106,10 +134,13 @@ struct AdmmPlan {
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
   unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
+  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged)
+  unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
   int ntiles_big = 0, ntiles_small = 0;
   int fin_elems = kElemChunk;
+  int hist_nv = 1;
 };
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
@@ -173,16 +204,21 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
   pl.hist_chunks.clear();
-  long long big_units = 0;
-  for (int i = 0; i < nprob; ++i) big_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kFinElems - 1) / kFinElems;
+  long long big_units = 0, hist_units = 0;
+  for (int i = 0; i < nprob; ++i) {
+    big_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kFinElems - 1) / kFinElems;
+    hist_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kHistElems - 1) / kHistElems;
+  }
   pl.fin_elems = big_units >= kFinMinUnits ? kFinElems : kElemChunk;
+  pl.hist_nv = hist_units > kHistMaxUnits ? 2 : 1;   // one round of resident stage-1 blocks
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
     const long long tot = (long long)d.I * d.ld;
     for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
-    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
-    pl.desc[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
+    const long long hu = (long long)kHistElems * pl.hist_nv;
+    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e});
+    pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
   }
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
@@ -190,6 +226,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_queue = cv.take<unsigned>(2);
+  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged);
+  pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
 }
@@ -223,6 +261,8 @@ struct QPlan {
   Chunk* d_pack = nullptr;
   Chunk* d_sse = nullptr;
   Chunk* d_hist = nullptr;
+  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged)
+  unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
 };
 
@@ -261,6 +301,8 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
   pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
+  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged);
+  pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
 }
@@ -292,11 +334,16 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
   if (qscheme == kMse) {
     const bool all = exhaustive || !two_stage_ok(ncand, bits);
-    if (!all && merged_ok(ncand, bits) && !g_legacy_stage1) {
-      launch_mse_prep2(nullptr, pl.d_jobs, n, ncand, bits, 0, s);
-      launch_mse_hist2(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+    std::vector<unsigned short> rank0, groups;
+    const bool merged = !all && merged_ok(ncand, bits) && !g_legacy_stage1 &&
+                        merged_tables(ncand, 1 << (bits - 1), rank0, groups);
+    if (merged) {
+      if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
+      if (!groups.empty() && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
+      launch_mse_hist3(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, pl.d_rank0,
+                       pl.d_groups, (int)groups.size() / 6, 1, s);
     } else if (!all) {
-      launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, s);
+      launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, 1, s);
     } else {   // exhaustive: every candidate's canonical SSE over all chunks
       launch_mse_select_all(nullptr, pl.d_jobs, n, ncand, 0, s);
       launch_mse_sse(nullptr, pl.d_jobs, pl.d_sse, (int)pl.sse_chunks.size(), ncand, bits, 0, s);
@@ -399,7 +446,14 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
-  const bool merged = merged_ok(num_attempts, bits) && !g_legacy_stage1;
+  std::vector<unsigned short> rank0, groups;
+  const bool merged = !exhaustive && merged_ok(num_attempts, bits) && !g_legacy_stage1 && qscheme == kMse &&
+                      merged_tables(num_attempts, 1 << (bits - 1), rank0, groups);
+  const int ngroups = (int)groups.size() / 6;
+  if (merged) {
+    if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
+    if (ngroups && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
+  }
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     prof_class(0); prof_mark(s);
@@ -409,10 +463,10 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
       prof_class(1); prof_mark(s);
       // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
-        launch_mse_prep2(pl.d_desc, nullptr, nprob, num_attempts, bits, slot, s);
-        launch_mse_hist2(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+        launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.d_rank0, pl.d_groups,
+                         ngroups, pl.hist_nv, s);
       } else if (!exhaustive) {
-        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, s);
+        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.hist_nv, s);
       } else {
         launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
         launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
@@ -431,8 +485,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 // diagnostics (not in include/admmq.h): per-workgroup timeline of the last GEMM launch
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
-int32_t admmq_debug_prep_trace(unsigned long long* host, int32_t n) { return copy_prep_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
+int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }
 
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
                                      int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,

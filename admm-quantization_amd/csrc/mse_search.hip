@@ -80,14 +80,60 @@ int copy_sel_stats(unsigned long long* host, int reset) {
   return 3;
 }
 
+// Closed form of level_threshold(s, k) (s > 0 normal, k >= 1): rint(fl(a/s)) >= k
+// <=> fl(a/s) >= H with H = k - 1/2 (k even: rint(H) = k) or H = next float above
+// k - 1/2 (k odd: the tie rounds down). fl(a/s) >= H <=> a/s >= m, the midpoint of
+// H and the float below it, where a/s == m rounds to H iff H's last mantissa bit is
+// 0 (round half to even). s * m is exact in fp64 (24 + 25 significant bits), so the
+// threshold is the smallest float >= s m, one float higher on a tie that rounds
+// down. Checked against level_threshold by admmq_debug_check_thresholds.
+__device__ __forceinline__ float level_threshold_fast(float s, int k) {
+  float H = (float)k - 0.5f;
+  if (k & 1) H = __uint_as_float(__float_as_uint(H) + 1u);
+  const float Hm = __uint_as_float(__float_as_uint(H) - 1u);
+  const double m = 0.5 * ((double)H + (double)Hm);
+  const double prod = (double)s * m;
+  float a = (float)prod;                                   // round to nearest
+  if ((double)a < prod) a = __uint_as_float(__float_as_uint(a) + 1u);
+  else if ((double)a > prod) {                             // nearest went up: is the float below still >= prod?
+    const float b = __uint_as_float(__float_as_uint(a) - 1u);
+    if ((double)b >= prod) a = b;
+  }
+  if ((double)a == prod && (__float_as_uint(H) & 1u)) a = __uint_as_float(__float_as_uint(a) + 1u);
+  return a;
+}
+
 // Threshold table of one job into LDS: thr[(k-1) n + c] = smallest a with
 // |q_c(a)| >= k, for k = 1..qmax (increasing in c and in k).
 __device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax) {
   const float den = (float)(2 * qmax - 1);
   for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
     const int k = 1 + e / n, c = e - (k - 1) * n;
-    thr[e] = level_threshold((2.0f * cand_t(mx, c, n)) / den, k);
+    thr[e] = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
   }
+}
+
+// Diagnostics: level_threshold_fast == level_threshold over random (s, k).
+__global__ void k_check_thresholds(unsigned seed, int nsamp, unsigned* mismatches) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
+    unsigned x = seed ^ (0x9E3779B9u * (unsigned)(i + 1));
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    const int k = 1 + (int)(x % 40u);
+    unsigned y = x * 2654435761u + 12345u;
+    y ^= y >> 13; y *= 0x5bd1e995u; y ^= y >> 15;
+    const float s = __uint_as_float((y & 0x007FFFFFu) | ((100u + (y >> 24) % 60u) << 23));   // s in [2^-27, 2^33)
+    if (level_threshold_fast(s, k) != level_threshold(s, k)) atomicAdd(mismatches, 1u);
+  }
+}
+int check_thresholds(unsigned seed, int nsamp) {
+  unsigned* d = nullptr;
+  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return -1;
+  hipMemset(d, 0, sizeof(unsigned));
+  hipLaunchKernelGGL(k_check_thresholds, dim3(256), dim3(256), 0, 0, seed, nsamp, d);
+  unsigned h = 0;
+  const bool ok = hipMemcpy(&h, d, sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess;
+  hipFree(d);
+  return ok ? (int)h : -1;
 }
 
 __device__ __forceinline__ int hist_fixed_exp(float mx, long long nelem, int qmax) {
@@ -226,7 +272,7 @@ __device__ void sse_in_block(const MseView& v, const int* lsel, int ncand, int b
 // 1024 threads x 4 elements per block; the block's histograms are flushed into one of
 // kHistRep replicas of the job's global histograms; the last block of the job to
 // finish (ticket) sums the replicas and runs the candidate selection.
-template <int QMAX>
+template <int QMAX, int NV>
 __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
                                                    const Chunk* __restrict__ chunks, int ncand, int slot, int abl) {
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
@@ -249,9 +295,13 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   __shared__ int last;
   // this thread's 4 elements: issued first, so the load overlaps the table setup
   const long long total = (long long)v.rows * v.ld;
-  const long long e = (long long)ck.start + 4LL * threadIdx.x;
-  float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < total) x4 = *reinterpret_cast<const float4*>(v.X + e);
+  float4 x4v[NV];   // NV float4 per thread: start + 4 tid + 4096 g
+#pragma unroll
+  for (int g = 0; g < NV; ++g) {
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * g;
+    x4v[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x4v[g] = *reinterpret_cast<const float4*>(v.X + e);
+  }
   fill_thresholds(thr, mx, n, QMAX);
   if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
   for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
@@ -268,10 +318,10 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   double s2 = 0.0;
   unsigned long long full1 = 0ull;
   unsigned full2 = 0u;
-  const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float x = xs[j];
+  for (int j = 0; j < 4 * NV; ++j) {
+    const float4 q4 = x4v[j >> 2];
+    const float x = (j & 3) == 0 ? q4.x : ((j & 3) == 1 ? q4.y : ((j & 3) == 2 ? q4.z : q4.w));
     s2 += (double)x * (double)x;
     const float a = __builtin_fabsf(x);
     const int cap = (x > 0.f) ? QMAX - 1 : QMAX;
@@ -389,84 +439,27 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// Stage 1, merged-threshold form (qmax * ncand <= kMaxMerged).
+// Stage 1, merged-threshold form (k_mse_hist3; qmax * ncand <= kMaxMerged).
 //
 // With B(a) = #{(k, c) : thr[k][c] <= a} over ALL levels and candidates and
 // L(k, c) = #{(k', c') : thr[k'][c'] <= thr[k][c]} (ties counted), for every a >= 0:
 //     a >= thr[k][c]  <=>  B(a) >= L(k, c).
-// So one binary search per element in the sorted merged table places it in bucket
-// B(|x|), and per candidate
+// So each element is placed once, in bucket B(|x|), and per candidate
 //     T1(c) = sum_k sum{ af : B >= L(k, c) },   T2(c) = sum_k (2k-1) #{ B >= L(k, c) }
 // over the elements allowed level k (x > 0 reaches at most qmax - 1, so the top level
-// reads the negatives' buckets only). These are the same integers as the per-level
-// breakpoint sums of k_mse_hist (each (element, level) pair contributes af once).
+// reads the negatives' buckets only): the same integers as the per-level breakpoint
+// sums of k_mse_hist (each (element, level) pair contributes af once).
 //
-// k_mse_prep2: per job and iteration, thr[k][c] -> sorted table tsort[M] and the
-// positions tpos[(k-1) n + c] = L(k, c) in [1, M] (one 1024-thread block per job).
-__device__ unsigned long long g_prep_trace[256][5];
-int copy_prep_trace(unsigned long long* host, int n) {
-  n = n < 256 ? n : 256;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prep_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess
-             ? n : -1;
-}
-
-__global__ __launch_bounds__(1024) void k_mse_prep2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                    int ncand, int bits, int slot) {
-  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
-  const MseView& v = mview(d, qj, blockIdx.x);
-  if (v.done && *v.done) return;
-  const float mx = __uint_as_float(v.stat[4 * slot]);
-  if (mse_degenerate(mx)) return;
-  __shared__ float thr[kMaxMerged];
-  const int n = ncand;
-  const int qmax = 1 << (bits - 1);
-  const int M = qmax * n;
-  fill_thresholds(thr, mx, n, qmax);
-  __syncthreads();
-  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
-  // Rank by counting (rows thr[j][.] are non-decreasing): with the total order
-  // (value, level, candidate), thr[k][c] has rank
-  //     sum_{j<k} #{c' : thr[j][c'] <= T} + c + sum_{j>k} #{c' : thr[j][c'] < T}
-  // and L(k, c) = sum_j #{c' : thr[j][c'] <= T}. Row counts start from the linear
-  // estimate t_c ~ S0 + c step (thr[j][c] ~ (2j-1) t_c / den) and walk to the exact one.
-  const float S0 = (float)(0.2 * (double)mx);
-  const float E0 = (float)(1.2 * (double)mx);
-  const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
-  const float den = (float)(2 * qmax - 1);
-  for (int e = threadIdx.x; e < M; e += blockDim.x) {
-    const int k = e / n, c = e - k * n;           // level k+1
-    const float T = thr[e];
-    int rank = c, L = 0;
-    for (int j = 0; j < qmax; ++j) {
-      const float* row = thr + j * n;
-      int le;                                        // #{c' : row[c'] <= T}
-      if (j == k) {
-        le = c + 1;
-        while (le < n && row[le] <= T) ++le;
-      } else {
-        const float tc = T * den / (float)(2 * j + 1);
-        const float ce = (tc - S0) * inv_step;
-        le = (ce < 0.f) ? 0 : (ce >= (float)n ? n : (int)ce + 1);
-        while (le < n && row[le] <= T) ++le;
-        while (le > 0 && row[le - 1] > T) --le;
-      }
-      L += le;
-      if (j < k) rank += le;
-      if (j > k) {
-        int lt = le;                                 // #{c' : row[c'] < T}
-        while (lt > 0 && row[lt - 1] == T) --lt;
-        rank += lt;
-      }
-    }
-    v.tpos[e] = (unsigned short)L;
-    v.tsort[rank] = T;
-  }
-  const unsigned long long T2 = T1;
-  if (threadIdx.x == 0 && blockIdx.x < 256) {
-    g_prep_trace[blockIdx.x][0] = T0; g_prep_trace[blockIdx.x][1] = T1; g_prep_trace[blockIdx.x][2] = T2;
-    g_prep_trace[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime(); g_prep_trace[blockIdx.x][4] = 0;
-  }
-}
+// The sorted order of the thresholds does not depend on mx: thr[k][c] is within a few
+// ulps of (2k-1) ((n-1) + 5c) * mx / (5 (n-1) den), an integer key whose distinct
+// values differ by >= 1.5e-5 relative for every supported (n, qmax). The host
+// computes that order once (rank0) with the groups of exactly equal keys; each block
+// scatters its thresholds by it, orders the tie groups by their actual values,
+// checks the result is non-decreasing (else ranks them by counting) and derives L.
+// A coarse index cnt[g] = #{thresholds in cells < g} over kCells equal cells of
+// [0, max threshold] then turns B(a) into two independent LDS reads and a walk of
+// the few thresholds of a's cell.
+constexpr int kCells = 2048;
 
 // Candidate selection from per-candidate totals T1/T2 (LDS) and S2, by one wave:
 // as select_wave, without the suffix scan.
@@ -519,9 +512,50 @@ __device__ void select_wave2(const MseView& v, int* sel, int* lsel, const unsign
   }
 }
 
-template <int QMAX>
-__global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                       const Chunk* __restrict__ chunks, int ncand, int slot) {
+
+// Rank-by-counting of the thresholds (fallback when the host order does not hold):
+// rows thr[j][.] are non-decreasing; with the order (value, level, candidate)
+// rank(k, c) = sum_{j<k} #{row j <= T} + c + sum_{j>k} #{row j < T}, L = sum_j #{row j <= T}.
+__device__ void rank_by_counting(const float* thr, float* tsort, unsigned short* L_out, float mx, int n, int qmax) {
+  const int M = qmax * n;
+  const float S0 = (float)(0.2 * (double)mx);
+  const float E0 = (float)(1.2 * (double)mx);
+  const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
+  const float den = (float)(2 * qmax - 1);
+  for (int e = threadIdx.x; e < M; e += blockDim.x) {
+    const int k = e / n, c = e - k * n;
+    const float T = thr[e];
+    int rank = c, L = 0;
+    for (int j = 0; j < qmax; ++j) {
+      const float* row = thr + j * n;
+      int le;
+      if (j == k) {
+        le = c + 1;
+        while (le < n && row[le] <= T) ++le;
+      } else {
+        const float ce = (T * den / (float)(2 * j + 1) - S0) * inv_step;
+        le = (ce < 0.f) ? 0 : (ce >= (float)n ? n : (int)ce + 1);
+        while (le < n && row[le] <= T) ++le;
+        while (le > 0 && row[le - 1] > T) --le;
+      }
+      L += le;
+      if (j < k) rank += le;
+      if (j > k) {
+        int lt = le;
+        while (lt > 0 && row[lt - 1] == T) --lt;
+        rank += lt;
+      }
+    }
+    L_out[e] = (unsigned short)L;
+    tsort[rank] = T;
+  }
+}
+
+template <int QMAX, int NV>
+__global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                      const Chunk* __restrict__ chunks, int ncand, int slot,
+                                                      const unsigned short* __restrict__ rank0,
+                                                      const unsigned short* __restrict__ groups, int ngroups) {
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   const Chunk ck = chunks[blockIdx.x];
   const MseView& v = mview(d, qj, ck.job);
@@ -540,53 +574,84 @@ __global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict
   unsigned long long* sumN = sumA + nb;
   unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
   unsigned* cntN = cntA + nb;
-  float* key = reinterpret_cast<float*>(cntN + nb);                          // M
-  unsigned short* tpos = reinterpret_cast<unsigned short*>(key + M);         // M
-  __shared__ double red[16];
-  __shared__ unsigned long long wtot[16], wtot2[16];
-  __shared__ unsigned wtot32[16], wtot32b[16];
+  float* thr = reinterpret_cast<float*>(cntN + nb);                          // M
+  float* tsort = thr + M;                                                    // M
+  unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
+  unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
+  __shared__ double red[8];
+  __shared__ unsigned long long wtot[8], wtot2[8];
+  __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
   const long long total = (long long)v.rows * v.ld;
-  float4 x4[2];
+  float4 x4[2 * NV];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {   // 8 elements: two float4 at start + 4 tid + 2048 hh
+  for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
     x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < total) x4[hh] = *reinterpret_cast<const float4*>(v.X + e);
   }
-  for (int i = threadIdx.x; i < M; i += blockDim.x) { key[i] = v.tsort[i]; tpos[i] = v.tpos[i]; }
+  fill_thresholds(thr, mx, n, QMAX);
+  for (int i = threadIdx.x; i < M; i += blockDim.x) rnk[i] = rank0[i];
   for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
+  __syncthreads();
+  for (int e = threadIdx.x; e < M; e += blockDim.x) tsort[rnk[e]] = thr[e];
+  __syncthreads();
+  for (int g = threadIdx.x; g < ngroups; g += blockDim.x) {   // exact-key ties: order by actual value
+    const unsigned short* gr = groups + 6 * g;
+    const int r0 = gr[0], m = gr[1];
+    int es[4];
+    float vs[4];
+    for (int j = 0; j < m; ++j) { es[j] = gr[2 + j]; vs[j] = thr[es[j]]; }
+    for (int i = 1; i < m; ++i)                                 // insertion sort, stable
+      for (int j = i; j > 0 && vs[j - 1] > vs[j]; --j) {
+        const float tv = vs[j]; vs[j] = vs[j - 1]; vs[j - 1] = tv;
+        const int te = es[j]; es[j] = es[j - 1]; es[j - 1] = te;
+      }
+    for (int j = 0; j < m; ++j) { tsort[r0 + j] = vs[j]; rnk[es[j]] = (unsigned short)(r0 + j); }
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int r = threadIdx.x; r + 1 < M; r += blockDim.x) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
+  if (__syncthreads_or(bad)) {
+    rank_by_counting(thr, tsort, rnk, mx, n, QMAX);   // never expected; exact either way
+  } else {
+    for (int e = threadIdx.x; e < M; e += blockDim.x) {   // L = 1 + index of the last equal value
+      const int r = rnk[e];
+      int l = r + 1;
+      while (l < M && tsort[l] == tsort[r]) ++l;
+      rnk[e] = (unsigned short)l;
+    }
+  }
+  __syncthreads();
+  // coarse index: cell(v) = min(kCells-1, (int)(v * inv)) is non-decreasing in v, so
+  // thresholds in cells below cell(a) are < a and those above are > a
+  const float inv = (float)kCells / tsort[M - 1];
+  for (int r = threadIdx.x; r < M; r += blockDim.x) {
+    const int cr = min(kCells - 1, (int)(tsort[r] * inv));
+    const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * inv));
+    for (int g = cp + 1; g <= cr; ++g) cell[g] = (unsigned short)r;
+    if (r == M - 1)
+      for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
+  }
   __syncthreads();
   const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
-  const float xs[8] = {x4[0].x, x4[0].y, x4[0].z, x4[0].w, x4[1].x, x4[1].y, x4[1].z, x4[1].w};
-  // binary searches of the 8 elements interleaved (independent LDS chains):
-  // lo = #{thresholds <= |x|}
-  int lo[8], hi[8];
-  float av[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { lo[j] = 0; hi[j] = M; av[j] = __builtin_fabsf(xs[j]); }
-  for (int step = M; step > 0; step >>= 1) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int mid = (lo[j] + hi[j]) >> 1;
-      const bool go = lo[j] < hi[j];
-      const bool le = key[min(mid, M - 1)] <= av[j];
-      lo[j] = (go && le) ? mid + 1 : lo[j];
-      hi[j] = (go && !le) ? mid : hi[j];
-    }
-  }
   double s2 = 0.0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float x = xs[j];
+  for (int j = 0; j < 8 * NV; ++j) {
+    const float4 q4 = x4[j >> 2];
+    const float x = (j & 3) == 0 ? q4.x : ((j & 3) == 1 ? q4.y : ((j & 3) == 2 ? q4.z : q4.w));
     s2 += (double)x * (double)x;
-    const int B = lo[j];                      // 0: reaches no level for any candidate
-    const bool live = B > 0;
+    const float a = __builtin_fabsf(x);
+    const int g = min(kCells - 1, (int)(a * inv));
+    int B = cell[g];
+    const int hiB = cell[g + 1];
+    while (B < hiB && tsort[B] <= a) ++B;       // B = #{thresholds <= a}
+    const bool live = B > 0;                    // 0: reaches no level for any candidate
     const int b = live ? B : dummy;
     const bool neg = x < 0.f;
-    const unsigned long long af = live ? to_fixed(av[j], K1) : 0ull;
+    const unsigned long long af = live ? to_fixed(a, K1) : 0ull;
     atomicAdd(neg ? &sumN[b] : &sumA[b], af);
     atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
   }
@@ -595,8 +660,8 @@ __global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict
   // all = positives + negatives; then suffix sums S[i] = sum over buckets >= i
   for (int i = threadIdx.x; i <= M; i += blockDim.x) { sumA[i] += sumN[i]; cntA[i] += cntN[i]; }
   __syncthreads();
-  {   // suffix sums S[i] = sum_{j >= i} of the four bucket arrays in one block pass:
-      // contiguous per-thread runs, then a scan of the run totals over the 1024 threads
+  {   // suffix sums of the four bucket arrays in one block pass: contiguous per-thread
+      // runs, then a scan of the run totals over the block (in thread order)
     const int len = M + 1;
     const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
     const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
@@ -636,11 +701,11 @@ __global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict
     unsigned long long t1 = 0ull, t2 = 0ull;
 #pragma unroll
     for (int k = 1; k < QMAX; ++k) {
-      const int L = tpos[(k - 1) * n + c];
+      const int L = rnk[(k - 1) * n + c];
       t1 += sumA[L];
       t2 += (unsigned long long)(2 * k - 1) * cntA[L];
     }
-    const int L = tpos[(QMAX - 1) * n + c];
+    const int L = rnk[(QMAX - 1) * n + c];
     t1 += sumN[L];
     t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
     if (t1) atomicAdd(&g1[c], t1);
@@ -697,10 +762,11 @@ __global__ __launch_bounds__(512, 8) void k_mse_hist2(const ProbDesc* __restrict
   trace(__builtin_amdgcn_s_memrealtime());
 }
 
-size_t hist2_lds_bytes(int ncand, int bits) {
+size_t hist3_lds_bytes(int ncand, int bits) {
   const size_t M = (size_t)ncand << (bits - 1);
   const size_t nb = M + 1 + 64;
-  return std::max(nb * (8 + 8 + 4 + 4) + M * 4 + ((M * 2 + 15) & ~(size_t)15), (size_t)kSseQuads * 16);
+  const size_t bytes = nb * (8 + 8 + 4 + 4) + M * 8 + (((M + 1) & ~(size_t)1) + kCells + 2) * 2;
+  return std::max((bytes + 15) & ~(size_t)15, (size_t)kSseQuads * 16);
 }
 
 size_t hist_lds_bytes(int ncand, int bits) {
@@ -772,36 +838,44 @@ __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d,
 }
 
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
-                     int slot, hipStream_t s) {
+                     int slot, int nv, hipStream_t s) {
   if (nchunks <= 0) return;
   const size_t lds = hist_lds_bytes(ncand, bits);
   static const int abl = getenv("ADMMQ_HIST_ABLATE") ? atoi(getenv("ADMMQ_HIST_ABLATE")) : 0;   // timing only
+#define ADMMQ_H1(Q, V) \
+  hipLaunchKernelGGL((k_mse_hist<Q, V>), dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl)
+#define ADMMQ_H1N(Q) if (nv == 2) ADMMQ_H1(Q, 2); else ADMMQ_H1(Q, 1)
   switch (bits) {
-    case 1: hipLaunchKernelGGL(k_mse_hist<1>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
-    case 2: hipLaunchKernelGGL(k_mse_hist<2>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
-    case 3: hipLaunchKernelGGL(k_mse_hist<4>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
-    case 4: hipLaunchKernelGGL(k_mse_hist<8>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
-    case 5: hipLaunchKernelGGL(k_mse_hist<16>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
-    default: hipLaunchKernelGGL(k_mse_hist<32>, dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl); break;
+    case 1: ADMMQ_H1N(1); break;
+    case 2: ADMMQ_H1N(2); break;
+    case 3: ADMMQ_H1N(4); break;
+    case 4: ADMMQ_H1N(8); break;
+    case 5: ADMMQ_H1N(16); break;
+    default: ADMMQ_H1N(32); break;
   }
+#undef ADMMQ_H1N
+#undef ADMMQ_H1
 }
 bool merged_ok(int ncand, int bits) {
-  return ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist2_lds_bytes(ncand, bits) <= 150 * 1024;
+  return ncand >= 2 && ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist3_lds_bytes(ncand, bits) <= 150 * 1024;
 }
-void launch_mse_prep2(const ProbDesc* d, const QJob* q, int njobs, int ncand, int bits, int slot, hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(k_mse_prep2, dim3(njobs), dim3(1024), 0, s, d, q, ncand, bits, slot);
-}
-void launch_mse_hist2(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
-                      int slot, hipStream_t s) {
+void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
+                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s) {
   if (nchunks <= 0) return;
-  const size_t lds = hist2_lds_bytes(ncand, bits);
+  const size_t lds = hist3_lds_bytes(ncand, bits);
+#define ADMMQ_H3(Q, V)                                                                                        \
+  hipLaunchKernelGGL((k_mse_hist3<Q, V>), dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot, rank0, \
+                     groups, ngroups)
+#define ADMMQ_H3N(Q) if (nv == 2) ADMMQ_H3(Q, 2); else ADMMQ_H3(Q, 1)
   switch (bits) {
-    case 1: hipLaunchKernelGGL(k_mse_hist2<1>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
-    case 2: hipLaunchKernelGGL(k_mse_hist2<2>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
-    case 3: hipLaunchKernelGGL(k_mse_hist2<4>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
-    case 4: hipLaunchKernelGGL(k_mse_hist2<8>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
-    default: hipLaunchKernelGGL(k_mse_hist2<16>, dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot); break;
+    case 1: ADMMQ_H3N(1); break;
+    case 2: ADMMQ_H3N(2); break;
+    case 3: ADMMQ_H3N(4); break;
+    case 4: ADMMQ_H3N(8); break;
+    default: ADMMQ_H3N(16); break;
   }
+#undef ADMMQ_H3N
+#undef ADMMQ_H3
 }
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {
   if (njobs > 0) hipLaunchKernelGGL(k_mse_select_all, dim3(njobs), dim3(64), 0, s, d, q, ncand, slot);

@@ -304,3 +304,12 @@ def test_als_short_fixture(torch_dev):
     W2 = _t(torch, dev, f2["w2_W"])
     run = factorize_layers([W2], [13], 3, 4, initial_factors=[[_t(torch, dev, f2["w2_A"]), _t(torch, dev, f2["w2_B"])]])[0]
     np.testing.assert_allclose(run.loss, z["w2_loss"], rtol=1e-3)
+
+
+def test_level_threshold_closed_form(torch_dev):
+    """The closed-form level threshold (fp64 midpoint) equals the IEEE-division
+    search it replaced, on 4M random (s, k)."""
+    from admmq import _lib
+    lib = _lib.load()
+    for seed in (1, 2, 3, 4):
+        assert lib.admmq_debug_check_thresholds(seed, 1 << 20) == 0

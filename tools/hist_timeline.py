@@ -46,7 +46,8 @@ for b in range(got):
 t0 = min(r[0] for r in rows)
 t1 = max(r[4] for r in rows)
 print(f"blocks {len(rows)}  span {(t1 - t0) / 100:.2f} us")
-for name, j0, j1 in (("setup", 0, 1), ("elements", 1, 2), ("scan+flush+ticket", 2, 3), ("select", 3, 4), ("total", 0, 4)):
+for name, j0, j1 in (("setup/tables", 0, 1), ("elements", 1, 2), ("scan+flush+ticket", 2, 3), ("select+stage2", 3, 4),
+                     ("total", 0, 4)):
     d = [(r[j1] - r[j0]) / 100 for r in rows]
     print(f"  {name:13s} avg {sum(d)/len(d):7.2f}  max {max(d):7.2f} us")
 starts = sorted((r[0] - t0) / 100 for r in rows)
@@ -57,7 +58,7 @@ for r in rows:
 print(f"  CUs used {len(cus)}; blocks per CU max {max(len(v) for v in cus.values())}")
 
 pb = (ctypes.c_ulonglong * (5 * 256))()
-gp = lib.admmq_debug_prep_trace(pb, 256)
+gp = lib.admmq_debug_prep_trace(pb, 256) if hasattr(lib, "admmq_debug_prep_trace") else 0
 pr = [[pb[5 * b + j] for j in range(5)] for b in range(gp)]
 pr = [r for r in pr if r[0] and r[3] >= r[0]]
 if pr:

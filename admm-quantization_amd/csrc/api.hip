@@ -48,6 +48,8 @@ struct Prof {
   std::vector<hipEvent_t> ev;
   std::vector<int> cls;
   size_t next = 0;
+  int every = 1;        // time one ADMM iteration in `every` (events add inter-kernel gaps)
+  bool sampled = true;  // the current iteration is timed
 };
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
@@ -91,11 +93,11 @@ static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, s
 }
 
 static inline void prof_mark(hipStream_t s) {
-  if (!g_prof.on || g_prof.next >= g_prof.ev.size()) return;
+  if (!g_prof.on || !g_prof.sampled || g_prof.next >= g_prof.ev.size()) return;
   (void)hipEventRecord(g_prof.ev[g_prof.next++], s);
 }
 static inline void prof_class(int c) {
-  if (g_prof.on && g_prof.next < g_prof.ev.size()) g_prof.cls.push_back(c);
+  if (g_prof.on && g_prof.sampled && g_prof.next < g_prof.ev.size()) g_prof.cls.push_back(c);
 }
 
 // Carves the workspace in a fixed order so that size and run agree exactly.
@@ -375,8 +377,11 @@ int32_t admmq_debug_set_legacy_stage1(int32_t enable) {
   return ADMMQ_OK;
 }
 
-int32_t admmq_profile_begin(int32_t max_launches) {
+int32_t admmq_profile_begin(int32_t max_launches, int32_t sample_every) {
   if (g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling already active");
+  if (sample_every < 1) return fail(ADMMQ_ERR_ARG, "sample_every must be >= 1");
+  g_prof.every = sample_every;
+  g_prof.sampled = true;
   g_prof.ev.resize(2 * (size_t)std::max(max_launches, 1));
   for (auto& e : g_prof.ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(ADMMQ_ERR_HIP, "hipEventCreate");
@@ -389,6 +394,7 @@ int32_t admmq_profile_begin(int32_t max_launches) {
 int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class) {
   if (!g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling not active");
   g_prof.on = false;
+  g_prof.sampled = true;
   for (int c = 0; c < 4; ++c) { ms_per_class[c] = 0.0; launches_per_class[c] = 0; }
   const size_t pairs = std::min(g_prof.next / 2, g_prof.cls.size());
   int rc = ADMMQ_OK;
@@ -456,6 +462,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   }
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
+    g_prof.sampled = it % g_prof.every == 0;
     prof_class(0); prof_mark(s);
     launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, slot, it, eps, num_attempts, s);
     prof_mark(s);
@@ -477,6 +484,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     launch_finalize_admm(pl.d_desc, pl.d_fin, nfin, pl.fin_elems, num_attempts, bits, qscheme, slot, it, s);
     prof_mark(s);
   }
+  g_prof.sampled = true;
   if (max_iter > 1) launch_unpack(pl.d_desc, nprob, pl.maxI, pl.maxR, s);
   if (info) hipLaunchKernelGGL(k_export_info, dim3((nprob + 63) / 64), dim3(64), 0, s, pl.d_desc, nprob, info);
   return check_hip("admm_run");

@@ -115,7 +115,28 @@ def algorithmic_flops(work, max_iter_admm, num_attempts=200):
     return sse, gemm
 
 
-def cpu_baseline(work, max_iter_admm, sample_iters=2):
+def gemm_bytes(work):
+    """Algorithmic HBM bytes of the solve GEMMs of one ADMM iteration over every mode:
+    P and U read, H_T and X = H_T - U written (4 I R floats) and M read (R^2 floats)."""
+    return sum(4.0 * (4 * d * R + R * R) for (s, W, R, _) in work for d in s.shape)
+
+
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_v3_traffic.json")
+
+
+def load_traffic():
+    """Per-launch HBM bytes of each launch class from the committed rocprofv3 PMC passes
+    (tools/traffic_json.py); PMC counters cannot be read live inside the timed region."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        t["file"] = os.path.relpath(TRAFFIC_FILE, os.path.dirname(os.path.abspath(__file__)))
+        return t
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(work, max_iter_admm, sample_iters=20):
     """torch-CPU port of the reference step (oracle/torch_port.py) on a bounded sample:
     every (layer, mode) of the workload, setup + `sample_iters` inner iterations timed,
     extrapolated linearly to max_iter_admm-1 iterations (per-iteration cost is constant
@@ -180,6 +201,8 @@ def main():
     ap.add_argument("--shard", choices=["replica", "layers"], default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
+    ap.add_argument("--prof-every", type=int, default=16,
+                    help="HIP-event timing of one ADMM iteration in N (an event pair per launch adds a gap)")
     ap.add_argument("--exhaustive", action="store_true",
                     help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
     a = ap.parse_args()
@@ -204,8 +227,8 @@ def main():
 
     prof = not a.no_profile
     if prof:
-        n_launch = a.steps * 3 * 3 * a.max_iter_admm + 64
-        _lib.check(lib.admmq_profile_begin(n_launch), "profile_begin")
+        n_launch = a.steps * 3 * 3 * (a.max_iter_admm // a.prof_every + 1) + 64
+        _lib.check(lib.admmq_profile_begin(n_launch, a.prof_every), "profile_begin")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -240,24 +263,36 @@ def main():
                           "mse_search": "exhaustive" if a.exhaustive else "two-stage exact"}}
         if kern is not None:
             sse_f, gemm_f = algorithmic_flops(work, a.max_iter_admm)
-            sse_f *= a.steps
-            gemm_f *= a.steps
-            ms = kern["ms"]
-            rf_sse = {"bound": "valu", "achieved": sse_f / (ms[1] * 1e-3) / 1e12, "peak": PEAK_F32,
-                      "unit": "TFLOP/s", "traffic": None}
-            rf_sse["frac"] = rf_sse["achieved"] / PEAK_F32
-            rf_gemm = {"bound": "mfma", "achieved": gemm_f / (ms[0] * 1e-3) / 1e12, "peak": PEAK_F32,
-                       "unit": "TFLOP/s", "traffic": None}
-            rf_gemm["frac"] = rf_gemm["achieved"] / PEAK_F32
-            dom = max(range(3), key=lambda k: ms[k])
-            out["roofline"] = rf_sse if dom == 1 else rf_gemm
-            out["roofline"]["kernel"] = ["k_gemm (solve, MFMA f32)", "MSE search (k_mse_hist/select/sse)",
-                                         "k_finalize_admm"][dom]
-            out["roofline_gemm"] = rf_gemm
-            out["kernel_ms_per_step"] = {"gemm": ms[0] / a.steps, "sse": ms[1] / a.steps,
-                                         "finalize": ms[2] / a.steps, "prepare": ms[3] / a.steps}
-            out["kernel_avg_us"] = {k: 1e3 * ms[i] / max(kern["launches"][i], 1)
-                                    for i, k in enumerate(["gemm", "sse", "finalize", "prepare"])}
+            ms, cnt = kern["ms"], kern["launches"]
+            # one ADMM iteration in prof_every is timed, uniformly over the modes, so the
+            # class's average launch duration is ms/cnt and its average algorithmic flops
+            # per launch is the step's total over all the step's launches
+            n_modes = max(len(s.shape) for (s, _, _, _) in work)
+            launches_per_step = n_modes * (a.max_iter_admm - 1)
+            avg_us = [1e3 * ms[i] / max(cnt[i], 1) for i in range(4)]
+            traffic = load_traffic()
+            rf = []
+            for cls, (flops, bound, name) in enumerate([
+                    (gemm_f, "mfma", "k_gemm (solve, MFMA f32)"),
+                    (sse_f, "valu", "MSE search (k_mse_hist3: stage 1 + selection + stage 2)")]):
+                ach = flops / launches_per_step / (avg_us[cls] * 1e-6) / 1e12 if cnt[cls] else 0.0
+                key = ["gemm", "sse"][cls]
+                r = {"bound": bound, "achieved": ach, "peak": PEAK_F32, "unit": "TFLOP/s", "frac": ach / PEAK_F32,
+                     "traffic": traffic["classes"][key]["bytes_per_launch"] if traffic else None,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "kernel": name,
+                     "launch_avg_us": avg_us[cls], "launches_timed": cnt[cls]}
+                if traffic:
+                    r["traffic_source"] = traffic["file"]
+                if cls == 0:
+                    r["algorithmic_bytes_per_launch"] = gemm_bytes(work) / n_modes
+                rf.append(r)
+            dom = max(range(3), key=lambda k: avg_us[k])
+            out["roofline"] = rf[1] if dom == 1 else rf[0]
+            out["roofline_gemm"] = rf[0]
+            out["kernel_ms_per_step"] = {k: avg_us[i] * 1e-3 * (launches_per_step if i < 3 else cnt[3] / a.steps)
+                                         for i, k in enumerate(["gemm", "sse", "finalize", "prepare"])}
+            out["kernel_avg_us"] = dict(zip(["gemm", "sse", "finalize", "prepare"], avg_us))
+            out["prof_every"] = a.prof_every
         if world == 1 and not a.no_cpu_baseline:
             # cpu_baseline leg: the CPU reference port timed on host cores, and the
             # metric's "rel-Frob err vs CPU ref" (oracle comparison of one ADMM step)

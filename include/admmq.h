@@ -101,9 +101,11 @@ int32_t admmq_set_exhaustive_search(int32_t enable);
 
 /* Optional HIP-event timing of every launch class issued by admmq_admm_prepare/run on
  * this thread between begin and end: class 0 GEMM (solve), 1 MSE candidate sweep,
- * 2 projection/dual update, 3 whole prepare phase. end() synchronises on the last event
+ * 2 projection/dual update, 3 whole prepare phase. Only ADMM iterations it with
+ * it % sample_every == 0 are timed (each event pair adds an inter-kernel gap, so the
+ * bench samples instead of timing every launch). end() synchronises on the last event
  * and returns summed milliseconds and launch counts per class (arrays of 4). */
-int32_t admmq_profile_begin(int32_t max_launches);
+int32_t admmq_profile_begin(int32_t max_launches, int32_t sample_every);
 int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */

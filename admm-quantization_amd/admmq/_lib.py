@@ -58,6 +58,7 @@ def load() -> ctypes.CDLL:
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
         "admmq_debug_set_legacy_stage1": (I32, [I32]),
+        "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
         "admmq_profile_end": (I32, [P, P]),
         "admmq_version": (I32, []),

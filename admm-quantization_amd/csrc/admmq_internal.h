@@ -24,8 +24,11 @@ constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaus
 constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
 constexpr int kMaxStage1Bits = 6;  // bits handled by the two-stage search (threshold table in LDS)
 constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms (atomic spread)
-constexpr int kMaxMerged = 4096;
-constexpr int kResRep = 8;         // replicas of the per-problem residual sums (atomic spread)   // qmax * ncand of the merged-threshold stage 1
+constexpr int kMaxMerged = 4096;   // qmax * ncand of the merged-threshold stage 1
+constexpr int kResRep = 8;         // replicas of the per-problem residual sums (atomic spread)
+constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU split-K solve
+constexpr int kThinCols = 256;     // ... columns per unit (64 lanes x float4)
+constexpr int kThinK = 128;        // ... reduction rows per unit (4 waves x 32)
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
@@ -63,6 +66,8 @@ struct ProbDesc {
   double* A64; double* L64; double* D64;   // D64: diagonal L blocks [nbk][32][32]
   MseView mv;
   double* res;
+  float* Part;     // thin factors (I <= kThinRows): split-K partial sums [nkg][NR][ld]
+  unsigned* tcnt;  // thin factors: arrival counter per 256-column block
   int* flags;
   float* rho;
   int I, R, ld, Ip, ldm, nbk;
@@ -83,6 +88,8 @@ struct QJob {
 
 // Work-unit tables (built on the host, uploaded once per call)
 struct GemmTile { int prob, tm, tn, first; };
+// Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
+struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
 struct Chunk { int job, start; };
 
 // float <-> order-preserving unsigned encodings for atomicMin/Max
@@ -99,12 +106,15 @@ void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
 void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
+void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
+                      int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
                  int slot, int iter, float eps, int ncand, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
+int copy_thin_trace(unsigned long long* host, int n);
 int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);

@@ -136,6 +136,10 @@ struct AdmmPlan {
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
   unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
+  std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
+  ThinUnit* d_thin = nullptr;
+  unsigned* d_tcnt = nullptr;    // their per-column-block arrival counters
+  int thin_nr = 0, ntcnt = 0;
   unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged)
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
@@ -145,11 +149,21 @@ struct AdmmPlan {
   int hist_nv = 1;
 };
 
+// Thin factors (I <= kThinRows) take the VALU split-K solve (k_gemm_thin) unless
+// ADMMQ_GEMM_THIN=0 (A/B: the 32 x 64 MFMA tiles instead).
+static bool thin_enabled() {
+  static const bool on = !(getenv("ADMMQ_GEMM_THIN") && std::string(getenv("ADMMQ_GEMM_THIN")) == "0");
+  return on;
+}
+
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
   if (nprob <= 0 || !probs) return fail(ADMMQ_ERR_ARG, "no problems");
   if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
   Carver cv(ws);
   pl.desc.resize(nprob);
+  pl.thin_nr = 0;
+  for (int i = 0; i < nprob; ++i)
+    if (thin_enabled() && probs[i].I > 0 && probs[i].I <= kThinRows) pl.thin_nr = std::max(pl.thin_nr, probs[i].I);
   for (int i = 0; i < nprob; ++i) {
     const admmq_problem& a = probs[i];
     if (a.I <= 0 || a.R <= 0) return fail(ADMMQ_ERR_ARG, "I and R must be positive");
@@ -172,6 +186,9 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.L64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.D64 = cv.take<double>((size_t)d.ldm * 32);
     d.res = cv.take<double>(2 * kResRep * 4);
+    const bool thin = pl.thin_nr > 0 && a.I <= kThinRows;
+    d.Part = thin ? cv.take<float>((size_t)((d.ld + kThinK - 1) / kThinK) * pl.thin_nr * d.ld) : nullptr;
+    d.tcnt = nullptr;
     d.flags = cv.take<int>(4);
     d.rho = cv.take<float>(4);
     carve_view(cv, d.mv, 2, ncand);
@@ -194,6 +211,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     const int bm = d.Ip == 32 ? 32 : 32 * gemm_big_wm();
+    if (pl.thin_nr > 0 && d.I <= kThinRows) continue;   // thin: k_gemm_thin units below
     std::vector<GemmTile>& dst = d.Ip == 32 ? small : pl.tiles;
     const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
     for (int g0 = 0; g0 < TN; g0 += 8)
@@ -203,6 +221,19 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.ntiles_big = (int)pl.tiles.size();
   pl.ntiles_small = (int)small.size();
   pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
+  // thin units, most reduction blocks first; counters: one per (problem, column block)
+  pl.thin.clear();
+  pl.ntcnt = 0;
+  std::vector<int> tcnt_off(nprob, -1);
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (!(pl.thin_nr > 0 && d.I <= kThinRows)) continue;
+    const int nkg = (d.ld + kThinK - 1) / kThinK, ncb = (d.ld + kThinCols - 1) / kThinCols;
+    tcnt_off[i] = pl.ntcnt;
+    pl.ntcnt += ncb;
+    for (int kg = 0; kg < nkg; ++kg)
+      for (int cb = 0; cb < ncb; ++cb) pl.thin.push_back({i, cb, kg, nkg, (cb == 0 && kg == 0) ? 1 : 0, {0, 0, 0}});
+  }
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
   pl.hist_chunks.clear();
@@ -228,6 +259,10 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_queue = cv.take<unsigned>(2);
+  pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
+  pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
+  for (int i = 0; i < nprob; ++i)
+    if (tcnt_off[i] >= 0 && pl.d_tcnt) pl.desc[i].tcnt = pl.d_tcnt + tcnt_off[i];
   pl.d_rank0 = cv.take<unsigned short>(kMaxMerged);
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
@@ -241,6 +276,7 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
+  if (!pl.thin.empty() && (rc = h2d(pl.d_thin, pl.thin.data(), pl.thin.size() * sizeof(ThinUnit), s))) return rc;
   return check_hip("upload");
 }
 
@@ -371,6 +407,15 @@ int32_t admmq_set_exhaustive_search(int32_t enable) {
   return ADMMQ_OK;
 }
 
+// diagnostics (not in include/admmq.h): workspace bytes of the plan carved against a
+// non-null base (no memory is touched), so a test can check that sizing (null base)
+// and the real carve agree
+size_t admmq_debug_admm_plan_bytes(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* base) {
+  AdmmPlan pl;
+  if (plan_admm(probs, nprob, num_attempts, base, pl) != ADMMQ_OK) return 0;
+  return pl.bytes;
+}
+
 // diagnostics (not in include/admmq.h): 1 = per-level stage 1, 0 = merged thresholds
 int32_t admmq_debug_set_legacy_stage1(int32_t enable) {
   g_legacy_stage1 = enable != 0;
@@ -449,6 +494,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
   if (hipMemsetAsync(pl.d_queue, 0, 2 * sizeof(unsigned), s) != hipSuccess) return check_hip("queue reset");
+  if (pl.ntcnt && hipMemsetAsync(pl.d_tcnt, 0, pl.ntcnt * sizeof(unsigned), s) != hipSuccess)
+    return check_hip("thin counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
@@ -465,6 +512,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     g_prof.sampled = it % g_prof.every == 0;
     prof_class(0); prof_mark(s);
     launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, slot, it, eps, num_attempts, s);
+    launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
     prof_mark(s);
     if (qscheme == kMse) {
       prof_class(1); prof_mark(s);
@@ -492,6 +540,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 
 // diagnostics (not in include/admmq.h): per-workgroup timeline of the last GEMM launch
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
+int32_t admmq_debug_thin_trace(unsigned long long* host, int32_t n) { return copy_thin_trace(host, n); }
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }

@@ -61,6 +61,19 @@ def test_workspace_planner(lib):
     assert b"positive" in lib.admmq_last_error()
 
 
+def test_workspace_size_matches_carve(lib):
+    """Sizing (null base) and the real carve (non-null base) must agree for every
+    mix of thin (I <= 16: split-K VALU solve), 32-row and tall factors."""
+    from admmq import _lib
+    shapes = [(9, 134), (9, 1141), (3, 40), (16, 700), (17, 300), (32, 64), (64, 134), (512, 1141)]
+    sets = [[s] for s in shapes] + [shapes, shapes[::-1], [(9, 134), (512, 1141)]]
+    for st in sets:
+        arr = _lib.problems_array([_lib.AdmmProblem(0, 0, 0, 0, 0, 0, 0, i, r) for i, r in st])
+        n = lib.admmq_admm_workspace_size(arr, len(st), 200)
+        assert n > 0
+        assert lib.admmq_debug_admm_plan_bytes(arr, len(st), 200, ctypes.c_void_p(1 << 20)) == n, st
+
+
 def test_quantize_planner(lib):
     from admmq import _lib
     t = _lib.QTensor(0, 0, 9, 134, 0.0, 0.0, 0, 0)

@@ -205,6 +205,28 @@ def test_reference_fixture_short_horizon(torch_dev):
     assert _rel(H.cpu().numpy(), z["w2_it3_H"]) < 1e-4
 
 
+@pytest.mark.parametrize("I,R", [(1, 40), (3, 300), (5, 129), (9, 700), (12, 257), (16, 1100), (17, 200)])
+def test_thin_factor_solve(torch_dev, I, R):
+    """Factors with I <= 16 rows take the VALU split-K solve (k_gemm_thin, exact row
+    count, 128-row reduction blocks summed by the last block to arrive); I = 17 takes
+    the 32-row MFMA tiles. One step vs the oracle, batched with a tall factor."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    rng = np.random.default_rng(I * 1000 + R)
+    probs, ref = [], []
+    for (i, r) in [(I, R), (64, 96)]:
+        B = rng.standard_normal((r, 2 * r)).astype(np.float32) / np.float32(np.sqrt(2 * r))
+        G = (B @ B.T + 0.5 * np.eye(r)).astype(np.float32)
+        F = rng.standard_normal((i, r)).astype(np.float32)
+        H0 = (rng.standard_normal((i, r)) * 0.1).astype(np.float32)
+        U0 = (rng.standard_normal((i, r)) * 0.01).astype(np.float32)
+        probs.append((_t(torch, dev, H0), _t(torch, dev, U0), _t(torch, dev, F), _t(torch, dev, G)))
+        ref.append(ao.admm_iteration(H0, U0, F, G, 2, 1e-8, 4, MSE, return_info=True)[2])
+    Hs, dbg = admm_iteration_batched(probs, 2, 1e-8, 4, MSE, debug_outputs=True)
+    for (HT, X), info in zip(dbg, ref):
+        assert _rel(HT.cpu().numpy(), info["HT"]) < 1e-5
+
+
 # ----------------------------------------------------------------------------- P3
 def test_batched_equals_single_and_deterministic(torch_dev):
     torch, dev = torch_dev
@@ -229,10 +251,13 @@ def test_batched_equals_single_and_deterministic(torch_dev):
         assert _bits_equal(b[0], a[0]) and _bits_equal(b[1], a[1])
 
 
-def test_iteration_count_and_early_exit(torch_dev):
+@pytest.mark.parametrize("layer,mode", [("layer1.0.conv1", 0), ("layer4.0.conv2", 2)])
+def test_iteration_count_and_early_exit(torch_dev, layer, mode):
+    """Mode 2 (I = 9) runs the thin split-K solve (k_gemm_thin): its stop test and
+    sticky break must match the MFMA tiles'."""
     torch, dev = torch_dev
     from admmq import admm_iteration_batched
-    H0, F, G = _layer_problem("layer1.0.conv1", 0)
+    H0, F, G = _layer_problem(layer, mode)
     mk = lambda: (_t(torch, dev, H0), torch.zeros(H0.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))  # noqa
     _, info = admm_iteration_batched([mk()], 7, 0.0, 4, MSE, return_info=True)
     assert info[0, 0].item() == 6 and info[0, 1].item() == 0

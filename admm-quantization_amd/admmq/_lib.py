@@ -35,6 +35,12 @@ class QTensor(ctypes.Structure):
                 ("has_minmax", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class CpLayer(ctypes.Structure):
+    _fields_ = [("W", ctypes.c_void_p), ("factors", ctypes.c_void_p * 3), ("G", ctypes.c_void_p),
+                ("F", ctypes.c_void_p), ("dims", ctypes.c_int32 * 3), ("ndim", ctypes.c_int32),
+                ("R", ctypes.c_int32)]
+
+
 _lib = None
 
 
@@ -61,6 +67,9 @@ def load() -> ctypes.CDLL:
         "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
         "admmq_profile_end": (I32, [P, P]),
+        "admmq_cp_workspace_size": (S, [P, I32, I32]),
+        "admmq_cp_gram_mttkrp": (I32, [P, I32, I32, P, S, P]),
+        "admmq_cp_rel_error": (I32, [P, I32, P, P, S, P]),
         "admmq_version": (I32, []),
         "admmq_last_error": (ctypes.c_char_p, []),
     }

@@ -28,35 +28,14 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import synthetic
-from .admm import admm_iteration_batched, init_factors, squared_relative_diff
+from .admm import admm_iteration_batched, init_factors
+from .als import gram_mttkrp, gram_mttkrp_batched, rel_error_batched  # noqa: F401
 from .quantization import quantize_batched
 
 
-def gram_mttkrp(W: torch.Tensor, factors: Sequence[torch.Tensor], mode: int):
-    """G (Gram∘Gram) and F (MTTKRP) of ``scripts/factorize.py:215-237`` / ``:276-287``.
-
-    F is computed as unfold(W, mode) @ KhatriRao(others) (one GEMM, no (I,J,R)
-    intermediate); G with the reference's own product order ``X^T X * (Y^T Y)``.
-    """
-    if W.dim() == 3:
-        A, B, C = factors
-        if mode == 0:
-            G = B.T @ B * (C.T @ C)
-            F = W.reshape(W.shape[0], -1) @ (B[:, None, :] * C[None, :, :]).reshape(-1, B.shape[1])
-        elif mode == 1:
-            G = A.T @ A * (C.T @ C)
-            F = W.permute(1, 0, 2).reshape(W.shape[1], -1) @ (A[:, None, :] * C[None, :, :]).reshape(-1, A.shape[1])
-        else:
-            G = A.T @ A * (B.T @ B)
-            F = W.permute(2, 0, 1).reshape(W.shape[2], -1) @ (A[:, None, :] * B[None, :, :]).reshape(-1, A.shape[1])
-        return G.contiguous(), F.contiguous()
-    A, B = factors
-    if mode == 0:
-        return (B.T @ B).contiguous(), (W @ B).contiguous()
-    return (A.T @ A).contiguous(), (W.T @ A).contiguous()
-
-
 def reconstruct(factors: Sequence[torch.Tensor]) -> torch.Tensor:
+    """[[factors]] as a dense tensor (torch; for callers that need the tensor itself -
+    the ALS driver's errors use the fused ``als.rel_error_batched`` instead)."""
     if len(factors) == 3:
         return torch.einsum('ir,jr,kr->ijk', *factors)
     return factors[0] @ factors[1].T
@@ -88,10 +67,8 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
     nmodes = max((len(r.factors) for r in act), default=0)
     for mode in range(nmodes):
         sel = [r for r in act if mode < len(r.factors)]
-        probs = []
-        for r in sel:
-            G, F = gram_mttkrp(r.W, r.factors, mode)
-            probs.append((r.factors[mode], r.duals[mode], F, G))
+        GF = gram_mttkrp_batched([(r.W, r.factors) for r in sel], mode)
+        probs = [(r.factors[mode], r.duals[mode], F, G) for r, (G, F) in zip(sel, GF)]
         Hs = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
                                     check_spd=False)
         for r, H in zip(sel, Hs):
@@ -101,9 +78,10 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
             r.quantized[mode] = q
     if not record_errors:
         return
-    for r in act:
-        r.loss.append(squared_relative_diff(r.W, reconstruct(r.factors)))
-        r.lossq.append(squared_relative_diff(r.W, reconstruct(r.quantized)))
+    errs = rel_error_batched([(r.W, r.factors) for r in act] + [(r.W, r.quantized) for r in act])
+    for n, r in enumerate(act):
+        r.loss.append(errs[n])
+        r.lossq.append(errs[len(act) + n])
         back = 5 if r.W.dim() == 3 else 10
         if len(r.loss) > 1 and abs(r.loss[-2] - r.loss[-1]) < tol:
             r.active = False
@@ -124,8 +102,9 @@ def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_
         run = LayerRun(names[i] if names else f"layer{i}", W, R, fs)
         if init != "random":   # scripts/factorize.py:192-204: record the starting point
             q = quantize_batched(fs, bits, qscheme, num_attempts=num_attempts)
-            run.loss.append(squared_relative_diff(W, reconstruct(fs)))
-            run.lossq.append(squared_relative_diff(W, reconstruct(q)))
+            e, eq = rel_error_batched([(W, fs), (W, q)])
+            run.loss.append(e)
+            run.lossq.append(eq)
         runs.append(run)
     for _ in range(max_iter_als):
         if not any(r.active for r in runs):
@@ -205,8 +184,7 @@ def main(argv=None):
     print('Factorization took {} minutes'.format((time.time() - start) / 60))
     for mode, factor in enumerate(factors):
         torch.save(factor.cpu(), os.path.join(outdir, fileprefix + f'_mode_{mode}.pt'))
-    error = squared_relative_diff(weight, reconstruct(factors))
-    qerror = squared_relative_diff(weight, reconstruct(factors_q))
+    error, qerror = rel_error_batched([(weight, factors), (weight, factors_q)])
     print('Factorization error is {} for usual and {} for quantized'.format(error, qerror))
     return factors, factors_q
 

@@ -101,6 +101,9 @@ __device__ __forceinline__ float dec_ord(unsigned e) {
   return __uint_as_float((e & 0x80000000u) ? (e & 0x7FFFFFFFu) : ~e);
 }
 
+// Records the thread's last error text (admmq_last_error) and returns `code`.
+int set_error(int code, const char* msg);
+
 // Host-side launchers (each defined in its own translation unit).
 void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);

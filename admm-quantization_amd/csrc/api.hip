@@ -17,6 +17,7 @@ static int fail(int code, const char* msg) {
   g_err = msg;
   return code;
 }
+int set_error(int code, const char* msg) { return fail(code, msg); }
 
 static int check_hip(const char* where) {
   const hipError_t e = hipGetLastError();

@@ -142,7 +142,6 @@ def cpu_baseline(work, max_iter_admm, sample_iters=20):
     extrapolated linearly to max_iter_admm-1 iterations (per-iteration cost is constant
     with eps=0)."""
     from oracle import torch_port
-    from admmq.factorize import gram_mttkrp
     total = 0.0
     n_fi = 0
     wall = time.time()
@@ -150,7 +149,7 @@ def cpu_baseline(work, max_iter_admm, sample_iters=20):
         Wc = W.cpu()
         fs = [f.cpu() for f in init]
         for m in range(len(s.shape)):
-            G, F = gram_mttkrp(Wc, fs, m)
+            G, F = torch_port.gram_mttkrp(Wc, fs, m)
             t0 = time.perf_counter()
             torch_port.admm_iteration(fs[m], torch.zeros_like(fs[m]), F, G, 1, 0.0, 4)
             t1 = time.perf_counter()

@@ -13,6 +13,10 @@
  *                                           incl. quantize_tensor_mse :118-144, min_max_quantize :48-66
  *   admmq_mse_sse_table                  <- source/quantization.py:129-141 (the candidate search, exposed
  *                                           for parity tests: canonical fixed-point SSE per candidate)
+ *   admmq_cp_gram_mttkrp                 <- scripts/factorize.py:215-237 (3-way) and :276-287 (2-way):
+ *                                           G = B.T @ B * (C.T @ C), F = torch.einsum('abc,cr,br->ar', W, C, B), ...
+ *   admmq_cp_rel_error                   <- scripts/factorize.py:246-253 + source/admm.py:14-15
+ *                                           squared_relative_diff(W, torch.einsum('ir,jr,kr->ijk', A, B, C))
  */
 #ifndef ADMMQ_H_
 #define ADMMQ_H_
@@ -107,6 +111,32 @@ int32_t admmq_set_exhaustive_search(int32_t enable);
  * and returns summed milliseconds and launch counts per class (arrays of 4). */
 int32_t admmq_profile_begin(int32_t max_launches, int32_t sample_every);
 int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class);
+
+/* One CP layer of the ALS sweep (scripts/factorize.py:207-310): W is dims[0] x dims[1]
+ * (x dims[2]) row-major (a 3x3 conv reshaped to (cout, cin, 9), or a 2-D weight);
+ * factors[d] is dims[d] x R row-major. G / F are outputs of admmq_cp_gram_mttkrp. */
+typedef struct admmq_cp_layer {
+  const float* W;
+  const float* factors[3]; /* factors[2] unused (NULL) when ndim == 2 */
+  float* G;                /* R x R: Hadamard product of the Grams of the factors other than `mode` */
+  float* F;                /* dims[mode] x R: MTTKRP of W with the Khatri-Rao product of the others */
+  int32_t dims[3];
+  int32_t ndim;            /* 2 or 3 */
+  int32_t R;
+} admmq_cp_layer;
+
+/* Workspace bytes for admmq_cp_gram_mttkrp (this mode) and admmq_cp_rel_error on these layers. */
+size_t admmq_cp_workspace_size(const admmq_cp_layer* layers, int32_t n, int32_t mode);
+
+/* For every layer: G = Gram∘Gram of the factors other than `mode` and F = the mode-`mode`
+ * MTTKRP (fp32 MFMA, deterministic split-K). factors[mode] is not read. */
+int32_t admmq_cp_gram_mttkrp(const admmq_cp_layer* layers, int32_t n, int32_t mode, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/* out[l] (device double[n]) = ||W - [[factors]]||_F / ||W||_F per layer, without
+ * materialising the reconstruction (fp32 MFMA products, fp64 sums). */
+int32_t admmq_cp_rel_error(const admmq_cp_layer* layers, int32_t n, double* out, void* workspace,
+                           size_t workspace_bytes, void* stream);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);

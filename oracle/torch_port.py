@@ -45,3 +45,26 @@ def admm_iteration(H, U, F, G, max_iter, eps, bits, num_attempts=200):
         if r < eps and s < eps:
             break
     return H, U
+
+
+def gram_mttkrp(W: torch.Tensor, factors, mode: int):
+    """Per-mode setup of scripts/factorize.py:215-237 (3-way) / :276-287 (2-way), in the
+    reference's own torch expressions (the einsum strings are the reference's)."""
+    if W.dim() == 3:
+        A, B, C = factors
+        if mode == 0:
+            return B.T @ B * (C.T @ C), torch.einsum('abc,cr,br->ar', W, C, B)
+        if mode == 1:
+            return A.T @ A * (C.T @ C), torch.einsum('abc,cr,ar->br', W, C, A)
+        return A.T @ A * (B.T @ B), torch.einsum('abc,br,ar->cr', W, B, A)
+    A, B = factors
+    if mode == 0:
+        return B.T @ B, W @ B
+    return A.T @ A, W.T @ A
+
+
+def rel_error(W: torch.Tensor, factors) -> float:
+    """squared_relative_diff(W, [[factors]]) (source/admm.py:14-15, scripts/factorize.py:246-253)."""
+    rec = torch.einsum('ir,jr,kr->ijk', *factors) if W.dim() == 3 else factors[0] @ factors[1].T
+    return torch.sqrt(torch.sum((W - rec) ** 2) / torch.sum(W ** 2)).item()
+

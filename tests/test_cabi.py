@@ -94,3 +94,40 @@ def test_product_path_refuses_cpu_tensors():
         quantize_tensor(x, 4, "channel_affine")
     with pytest.raises(NotImplementedError):
         quantize_tensor(x, 4, "tensor_log")
+
+
+def test_cp_layer_struct_and_planner(lib):
+    """admmq_cp_layer layout and the ALS-contraction workspace planner (no compute)."""
+    from admmq import _lib
+    assert ctypes.sizeof(_lib.CpLayer) == 8 + 3 * 8 + 8 + 8 + 3 * 4 + 4 + 4 + 4   # + tail pad to 8
+
+    def layer(dims, R):
+        L = _lib.CpLayer()
+        L.W = 0x1000
+        for d in range(3):
+            L.factors[d] = 0x2000 * (d + 1) if d < len(dims) else None
+            L.dims[d] = dims[d] if d < len(dims) else 0
+        L.ndim, L.R = len(dims), R
+        return L
+
+    arr = (_lib.CpLayer * 2)(layer((512, 512, 9), 1141), layer((2048, 512), 204))
+    for mode in range(2):
+        n = lib.admmq_cp_workspace_size(arr, 2, mode)
+        assert n > 0
+    # mode 2 of the 3x3 conv: K = 512*512 split into chunks -> partial planes (9 x 1141 each)
+    one = (_lib.CpLayer * 1)(layer((512, 512, 9), 1141))
+    assert lib.admmq_cp_workspace_size(one, 1, 2) > 2 * 9 * 1141 * 4
+    bad = (_lib.CpLayer * 1)(layer((4, 5, 6), 3))
+    bad[0].ndim = 4
+    assert lib.admmq_cp_workspace_size(bad, 1, 0) == 0
+
+
+def test_als_contractions_refuse_cpu_tensors():
+    import torch
+    from admmq.als import gram_mttkrp, rel_error
+    W = torch.randn(4, 5, 6)
+    fs = [torch.randn(n, 3) for n in W.shape]
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        gram_mttkrp(W, fs, 0)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        rel_error(W, fs)

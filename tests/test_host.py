@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from admmq import synthetic
-from admmq.factorize import gram_mttkrp, reconstruct
+from admmq.factorize import reconstruct
+from oracle import torch_port
 from oracle import admm_oracle as ao
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -36,19 +37,20 @@ def test_resnet50_ranks_match_reference_table():
         assert got[k] == v, k
 
 
-def test_gram_mttkrp_matches_einsum():
+def test_torch_port_gram_mttkrp_matches_oracle():
+    """The CPU baseline's per-mode setup (reference expressions) vs the numpy oracle."""
     rng = np.random.default_rng(0)
     W = torch.from_numpy(rng.standard_normal((6, 5, 4)).astype(np.float32))
     fs = [torch.from_numpy(rng.standard_normal((n, 3)).astype(np.float32)) for n in W.shape]
     specs = ["abc,cr,br->ar", "abc,cr,ar->br", "abc,br,ar->cr"]
     args = [(fs[2], fs[1]), (fs[2], fs[0]), (fs[1], fs[0])]
     for m in range(3):
-        G, F = gram_mttkrp(W, fs, m)
+        G, F = torch_port.gram_mttkrp(W, fs, m)
         torch.testing.assert_close(F, torch.einsum(specs[m], W, *args[m]), rtol=1e-5, atol=1e-5)
         Gn, Fn = ao.gram_mttkrp(W.numpy(), [f.numpy() for f in fs], m)
         np.testing.assert_allclose(G.numpy(), Gn, rtol=1e-6)
     W2 = torch.from_numpy(rng.standard_normal((6, 5)).astype(np.float32))
-    G, F = gram_mttkrp(W2, fs[:2], 1)
+    G, F = torch_port.gram_mttkrp(W2, fs[:2], 1)
     torch.testing.assert_close(F, W2.T @ fs[0])
     assert reconstruct(fs[:2]).shape == (6, 5)
 

@@ -87,7 +87,9 @@ struct QJob {
 };
 
 // Work-unit tables (built on the host, uploaded once per call)
-struct GemmTile { int prob, tm, tn, first; };
+// GEMM tile: rows tm, columns tn of problem prob, K-steps [k0, k0 + nk). part >= 0: one
+// half (ks = 0 / 1) of a split-K pair, whose second-arriving half finishes the tile.
+struct GemmTile { int prob, tm, tn, first, k0, nk, part, ks; };
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
 struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
 struct Chunk { int job, start; };
@@ -112,7 +114,8 @@ void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s)
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
                       int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
-                 int slot, int iter, float eps, int ncand, hipStream_t s);
+                 float* kpart, unsigned* pcnt, int slot, int iter, float eps, int ncand, hipStream_t s);
+int gemm_split_min_steps();
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);

@@ -1,6 +1,8 @@
 // C-ABI of libadmmq: workspace planning and stream-ordered launch sequences.
 // See include/admmq.h for the contract and the reference interfaces replaced.
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -55,6 +57,8 @@ struct Prof {
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
+// Big GEMM tiles placed by whole layers per XCD (ADMMQ_GEMM_XCD=1; default: the column-interleaved order).
+static bool g_xcd_layers = getenv("ADMMQ_GEMM_XCD") && atoi(getenv("ADMMQ_GEMM_XCD")) != 0;
 // Stage-1 form: merged thresholds (k_mse_hist3, default where supported) or per-level
 // (k_mse_hist; ADMMQ_STAGE1=legacy, and wherever merged_tables/merged_ok decline). Both
 // give the same integers.
@@ -137,6 +141,9 @@ struct AdmmPlan {
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
   unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
+  int nsplit = 0;                // split-K tile pairs
+  float* d_kpart = nullptr;      // [nsplit][2][64 x 64] partial sums
+  unsigned* d_pcnt = nullptr;    // [nsplit] arrival counters (zeroed per run)
   std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
   ThinUnit* d_thin = nullptr;
   unsigned* d_tcnt = nullptr;    // their per-column-block arrival counters
@@ -155,6 +162,77 @@ struct AdmmPlan {
 static bool thin_enabled() {
   static const bool on = !(getenv("ADMMQ_GEMM_THIN") && std::string(getenv("ADMMQ_GEMM_THIN")) == "0");
   return on;
+}
+
+static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
+  GemmTile t;
+  t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.k0 = 0; t.nk = nk; t.part = -1; t.ks = 0;
+  return t;
+}
+
+// Whole-layer XCD placement of the big GEMM tiles. Workgroup b runs on XCD b % 8
+// (round-robin dispatch; every tile of a launch is resident at once), and an XCD's
+// L2 serves its workgroups only: a layer whose tiles are spread over all 8 XCDs is
+// fetched from the Infinity Cache 8 times (P once per XCD, M once per column slab),
+// one kept on one XCD about once. Layers are cut into column-tile ranges of at most
+// an eighth of the launch's MFMA work and placed largest first on the least-loaded
+// XCD (LPT); each XCD's list runs longest K first, tm-major within a column group.
+// Position p of the table takes the next tile of XCD p % 8 (another XCD's when that
+// list has run out).
+static void order_tiles_by_xcd(AdmmPlan& pl, const std::vector<int>& order) {
+  struct Piece { int prob, tn0, tn1; double work; };
+  std::vector<Piece> pieces;
+  double total = 0.0;
+  const int bm = 32 * gemm_big_wm();
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip == 32) continue;
+    total += (double)(d.Ip / bm) * ((d.ld + 63) / 64) * d.ld;
+  }
+  const double cap = total / 8.0;
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip == 32) continue;
+    const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
+    const double col_work = (double)TM * d.ld;
+    const int npieces = std::max(1, (int)std::ceil(col_work * TN / cap - 1e-9));
+    for (int q = 0; q < npieces; ++q) {
+      const int a = TN * q / npieces, b = TN * (q + 1) / npieces;
+      if (b > a) pieces.push_back({i, a, b, col_work * (b - a)});
+    }
+  }
+  std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& x, const Piece& y) { return x.work > y.work; });
+  std::vector<std::vector<GemmTile>> lists(8);
+  double load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  std::vector<std::vector<Piece>> own(8);
+  for (const Piece& pc : pieces) {
+    const int x = (int)(std::min_element(load, load + 8) - load);
+    load[x] += pc.work;
+    own[x].push_back(pc);
+  }
+  for (int x = 0; x < 8; ++x) {
+    std::stable_sort(own[x].begin(), own[x].end(),
+                     [&](const Piece& a, const Piece& b) { return pl.desc[a.prob].ld > pl.desc[b.prob].ld; });
+    for (const Piece& pc : own[x]) {
+      const ProbDesc& d = pl.desc[pc.prob];
+      const int TM = d.Ip / bm;
+      for (int g0 = pc.tn0; g0 < pc.tn1; g0 += 8)
+        for (int tm = 0; tm < TM; ++tm)
+          for (int tn = g0; tn < std::min(pc.tn1, g0 + 8); ++tn)
+            lists[x].push_back(mk_tile(pc.prob, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+    }
+  }
+  size_t n = 0, pos[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (auto& l : lists) n += l.size();
+  for (size_t p = 0; p < n; ++p) {
+    int x = (int)(p % 8);
+    if (pos[x] >= lists[x].size()) {   // this XCD's list is done: take from the longest remaining one
+      size_t best = 0;
+      for (int y = 0; y < 8; ++y)
+        if (lists[y].size() - pos[y] > best) { best = lists[y].size() - pos[y]; x = y; }
+    }
+    pl.tiles.push_back(lists[x][pos[x]++]);
+  }
 }
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
@@ -205,19 +283,52 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
-  // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
-  // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
-  // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
   std::vector<GemmTile> small;
-  for (int i : order) {
+  if (g_xcd_layers) {
+    order_tiles_by_xcd(pl, order);
+  } else {
+    // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
+    // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
+    // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      const int bm = d.Ip == 32 ? 32 : 32 * gemm_big_wm();
+      if (pl.thin_nr > 0 && d.I <= kThinRows) continue;   // thin: k_gemm_thin units below
+      if (d.Ip == 32) continue;
+      const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
+      for (int g0 = 0; g0 < TN; g0 += 8)
+        for (int tm = 0; tm < TM; ++tm)
+          for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
+            pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+    }
+  }
+  // Split-K: a big tile of >= gemm_split_min_steps() K-steps becomes two halves (one
+  // workgroup each; partial pair `part`), so the grid's work units are of similar
+  // length and the hardware's dispatch of the tail balances the CUs; units then run
+  // longest first (stable: the XCD-aware order within equal lengths).
+  pl.nsplit = 0;
+  if (gemm_split_min_steps() > 0) {
+    std::vector<GemmTile> out;
+    out.reserve(pl.tiles.size() * 2);
+    std::vector<GemmTile> second;
+    for (const GemmTile& t : pl.tiles) {
+      if (t.nk < gemm_split_min_steps()) { out.push_back(t); continue; }
+      GemmTile a = t, b = t;
+      a.nk = t.nk / 2; a.part = pl.nsplit; a.ks = 0;
+      b.k0 = a.nk; b.nk = t.nk - a.nk; b.part = pl.nsplit; b.ks = 1; b.first = 0;
+      ++pl.nsplit;
+      out.push_back(a);
+      second.push_back(b);
+    }
+    out.insert(out.end(), second.begin(), second.end());
+    std::stable_sort(out.begin(), out.end(), [](const GemmTile& x, const GemmTile& y) { return x.nk > y.nk; });
+    pl.tiles.swap(out);
+  }
+  for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
-    const int bm = d.Ip == 32 ? 32 : 32 * gemm_big_wm();
-    if (pl.thin_nr > 0 && d.I <= kThinRows) continue;   // thin: k_gemm_thin units below
-    std::vector<GemmTile>& dst = d.Ip == 32 ? small : pl.tiles;
-    const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
-    for (int g0 = 0; g0 < TN; g0 += 8)
-      for (int tm = 0; tm < TM; ++tm)
-        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn) dst.push_back({i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0});
+    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip != 32) continue;
+    const int TN = (d.ld + 63) / 64;
+    for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
   }
   pl.ntiles_big = (int)pl.tiles.size();
   pl.ntiles_small = (int)small.size();
@@ -260,6 +371,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_queue = cv.take<unsigned>(2);
+  pl.d_kpart = cv.take<float>((size_t)std::max(pl.nsplit, 1) * 2 * 64 * 64);
+  pl.d_pcnt = cv.take<unsigned>(std::max(pl.nsplit, 1));
   pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
   pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
   for (int i = 0; i < nprob; ++i)
@@ -495,6 +608,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
   if (hipMemsetAsync(pl.d_queue, 0, 2 * sizeof(unsigned), s) != hipSuccess) return check_hip("queue reset");
+  if (pl.nsplit && hipMemsetAsync(pl.d_pcnt, 0, pl.nsplit * sizeof(unsigned), s) != hipSuccess)
+    return check_hip("split counter reset");
   if (pl.ntcnt && hipMemsetAsync(pl.d_tcnt, 0, pl.ntcnt * sizeof(unsigned), s) != hipSuccess)
     return check_hip("thin counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
@@ -512,7 +627,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     prof_class(0); prof_mark(s);
-    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, slot, it, eps, num_attempts, s);
+    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, pl.d_kpart, pl.d_pcnt, slot, it,
+                eps, num_attempts, s);
     launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
     prof_mark(s);
     if (qscheme == kMse) {

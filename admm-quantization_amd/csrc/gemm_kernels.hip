@@ -90,7 +90,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // workgroup's K-loop ends. Every launch draws exactly ntiles tickets (each workgroup's
 // last draw fails), so launch number `iter` of a run owns tickets
 // [iter * ntiles, (iter + 1) * ntiles) and the counter is zeroed once per run. With
-// gridDim.x == ntiles (the default) every workgroup runs exactly one tile.
+// gridDim.x == ntiles (the default) every workgroup runs exactly one tile and draws no ticket.
 //
 // Workgroup tile (32 WM) x 64 with 2 WM KS waves: the KS waves (ks, wm, wn) own the
 // 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
@@ -98,8 +98,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // fixed order at the end.
 template <int WM, int KS, int NS>
 __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
-                                                        int ntiles, unsigned* __restrict__ queue, int slot, int iter,
-                                                        float eps, int ncand) {
+                                                        int ntiles, unsigned* __restrict__ queue,
+                                                        float* __restrict__ kpart, unsigned* __restrict__ pcnt, int slot,
+                                                        int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
   constexpr int NSUB = 2 * WM;                 // 32 x 32 sub-tiles per workgroup
   constexpr int NW = NSUB * KS;                // waves
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
   __shared__ __attribute__((aligned(16))) float st4[NS > 4 ? STAGE : 4];
   __shared__ __attribute__((aligned(16))) float st5[NS > 5 ? STAGE : 4];
   float* const stp[6] = {st0, st1, st2, st3, st4, st5};
-  __shared__ int s_next;
+  __shared__ int s_next, s_last;
   __shared__ unsigned red[3][NSUB];
 
   const int tid = threadIdx.x;
@@ -135,6 +136,8 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
   const int swz = (i >> 1) & 7;
   const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * wn + i) * 32;
   const unsigned base = (unsigned)iter * (unsigned)ntiles;
+  // one workgroup per tile (the default grid): no ticket queue, no returning atomic per tile
+  const bool one_each = (int)gridDim.x >= ntiles;
 
   for (int t = blockIdx.x; t < ntiles;) {
     const unsigned long long t_tile = __builtin_amdgcn_s_memrealtime();
@@ -145,9 +148,9 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
       if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
       skip = true;
     }
-    if (skip && tid == 0) s_next = (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+    if (skip && tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
     if (!skip) {
-      if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+      if (tl.first && tl.ks == 0) {   // this iteration's quantizer-search accumulators start at zero
         unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
         unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
         unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
       }
       const int ld = p.ld, ldm = p.ldm;
       const int row0 = tl.tm * BM, col0 = tl.tn * BN;
-      const int nk = ld / BK;
+      const int nk = tl.nk;
 
       // per-lane global source of each of this wave's glds pieces (K-step 0)
       const float* src[GPW];
@@ -166,8 +169,8 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
         const int g = wave * GPW + j;
         const int r = 8 * g + (lane >> 3);                       // image row
         const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
-        src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + 4 * c
-                          : p.M + (size_t)(col0 + r - BM) * ldm + 4 * c;
+        src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
+                          : p.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
       }
 #define ADMMQ_ISSUE(s, kt)                                                 \
   _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
 #undef ADMMQ_ISSUE
       // next ticket, drawn once this tile's K-loop is done (its latency hides behind
       // the epilogue; drawing earlier would hand tiles out before workers are free)
-      if (tid == 0) s_next = (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+      if (tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
       __syncthreads();   // nothing in flight any more; the stages may be reused
       if (KS > 1) {      // fixed-order reduction of the KS partial accumulators (deterministic)
         if (ks > 0) {
@@ -234,8 +237,35 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
         }
       }
 
+      // split-K pair: publish this half (agent-scope stores write through the XCD L2);
+      // the half whose arrival is second (odd count: two arrivals per pair per launch,
+      // counters zeroed per run) adds the other's partial and runs the epilogue. The
+      // sum of two terms is the same in either arrival order.
+      bool fin = true;
+      if (tl.part >= 0) {
+        float* mine = kpart + ((size_t)tl.part * 2 + tl.ks) * (NSUB * 1024);
+        if (ks == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __hip_atomic_store(mine + (sub * 16 + r) * 64 + lane, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0)
+          s_last = (int)(__hip_atomic_fetch_add(pcnt + tl.part, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u);
+        __syncthreads();
+        fin = s_last != 0;
+        if (fin) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other half's stores are visible
+          if (ks == 0) {
+            const float* other = kpart + ((size_t)tl.part * 2 + (tl.ks ^ 1)) * (NSUB * 1024);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += ldg(other + (sub * 16 + r) * 64 + lane);
+          }
+        }
+      }
       // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-      if (ks == 0) {
+      if (ks == 0 && fin) {
         const int col = col0 + 32 * wn + i;
         unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
         if (col < ld) {
@@ -259,7 +289,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
         if (lane == 0) { red[0][sub] = amax; red[1][sub] = mn; red[2][sub] = mxo; }
       }
       __syncthreads();
-      if (tid == 0) {
+      if (tid == 0 && fin) {
         unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
 #pragma unroll
         for (int w = 1; w < NSUB; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
@@ -540,8 +570,14 @@ int gemm_big_wm() {
 // Workgroups per CU for the persistent grid (MI355X: 256 CUs)
 static int gemm_grid(int ntiles, int per_cu) { return std::min(ntiles, 256 * per_cu); }
 
+// Tiles with at least this many K-steps are split into two K halves (0: never).
+int gemm_split_min_steps() {
+  static const int v = env_int("ADMMQ_GEMM_SPLIT", 0);
+  return v;
+}
+
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
-                 int slot, int iter, float eps, int ncand, hipStream_t s) {
+                 float* kpart, unsigned* pcnt, int slot, int iter, float eps, int ncand, hipStream_t s) {
   // tiles[0 .. ntiles_big) are (32 WM)x64, then ntiles_small 32x64 tiles (WM=1);
   // queue[0] / queue[1] are their ticket counters.
   static const int cfg_big = env_int("ADMMQ_GEMM_BIG", 13);     // KS*10 + NS
@@ -549,13 +585,16 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
   static const int per_cu = env_int("ADMMQ_GEMM_PER_CU", 0);    // 0: one workgroup per tile
 #define ADMMQ_GEMM(WM, KS, NS, n, t, q)                                                                      \
   hipLaunchKernelGGL((k_gemm<WM, KS, NS>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, d, \
-                     t, n, q, slot, iter, eps, ncand)
+                     t, n, q, kpart, pcnt, slot, iter, eps, ncand)
   if (ntiles_big > 0) {
     if (gemm_big_wm() == 4) {
       ADMMQ_GEMM(4, 1, 3, ntiles_big, tiles, queue);
     } else {
       switch (cfg_big) {
         case 14: ADMMQ_GEMM(2, 1, 4, ntiles_big, tiles, queue); break;
+        case 15: ADMMQ_GEMM(2, 1, 5, ntiles_big, tiles, queue); break;
+        case 16: ADMMQ_GEMM(2, 1, 6, ntiles_big, tiles, queue); break;
+        case 24: ADMMQ_GEMM(2, 2, 4, ntiles_big, tiles, queue); break;
         case 23: ADMMQ_GEMM(2, 2, 3, ntiles_big, tiles, queue); break;
         case 12: ADMMQ_GEMM(2, 1, 2, ntiles_big, tiles, queue); break;
         default: ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles, queue); break;

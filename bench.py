@@ -2,6 +2,7 @@
 """ADMM quantized CP factorization benchmark (BASELINE.json metric, config C3).
 
 A step = one ALS sweep of scripts/factorize.py over all 16 resnet18 3x3 convs
+(default; `--model resnet50` / `llama7b` run configs C4 / C5)
 (4-bit tensor_mseminmax_symmetric, reduction rate 2.0): for each mode A, B, C the
 Gram∘Gram / MTTKRP, one batched admm_iteration with max_iter_admm=1000 (999 inner
 iterations, eps=0 so no early exit), the re-quantization, then the two
@@ -50,6 +51,19 @@ def lpt(specs, nranks):
         owner[i] = r
         loads[r] += layer_cost(specs[i], specs[i].rank())
     return owner
+
+
+CONFIG_ID = {"resnet18": "C3", "resnet50": "C4", "llama7b": "C5"}
+
+
+def workload_name(model, work, max_iter_admm):
+    """BASELINE.json config the run measures: C3 resnet18 16 3x3 convs (3-way), C4 resnet50
+    48 convs (3x3 -> 3-way, 1x1 -> 2-way), C5 one Llama-7B decoder layer (7 2-way matrices)."""
+    n3 = sum(1 for (s, _, _, _) in work if len(s.shape) == 3)
+    n2 = len(work) - n3
+    kinds = ", ".join(k for k in (f"{n3} 3-way (3x3 conv)" if n3 else "", f"{n2} 2-way" if n2 else "") if k)
+    return (f"{CONFIG_ID.get(model, model)}: {model} {len(work)} layers per GPU ({kinds}), 1 ALS sweep x all modes x "
+            f"{max_iter_admm - 1} ADMM iters (eps=0), 4-bit mse-minmax, rate 2.0")
 
 
 def build_workload(model, rank, world, shard, device):
@@ -199,6 +213,8 @@ def main():
     ap.add_argument("--max-iter-admm", type=int, default=1000)
     ap.add_argument("--shard", choices=["replica", "layers"], default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-iters", type=int, default=None,
+                    help="inner iterations timed per (layer, mode) on the CPU (default 20; 1 for llama7b)")
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP-event timing of one ADMM iteration in N (an event pair per launch adds a gap)")
@@ -254,8 +270,7 @@ def main():
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * elapsed_max / a.steps,
                "higher_is_better": True, "scaling": "weak" if a.shard == "replica" else "strong",
                "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-               "config": {"workload": f"C3: {a.model} {len(work)} 3x3 convs per GPU, 1 ALS sweep x 3 modes x "
-                                      f"{a.max_iter_admm - 1} ADMM iters (eps=0), 4-bit mse-minmax, rate 2.0",
+               "config": {"workload": workload_name(a.model, work, a.max_iter_admm),
                           "factor_iterations_per_step_per_gpu": fi_per_step, "max_iter_admm": a.max_iter_admm,
                           "parallelism": f"{'replica' if a.shard == 'replica' else 'layer-shard'} x{world}, "
                                          "one RCCL gather of factors per step",
@@ -295,7 +310,8 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             # cpu_baseline leg: the CPU reference port timed on host cores, and the
             # metric's "rel-Frob err vs CPU ref" (oracle comparison of one ADMM step)
-            out["cpu_baseline"] = cpu_baseline(work, a.max_iter_admm)
+            si = a.cpu_sample_iters if a.cpu_sample_iters is not None else (1 if a.model == "llama7b" else 20)
+            out["cpu_baseline"] = cpu_baseline(work, a.max_iter_admm, sample_iters=si)
             out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             try:
                 rel, exact = parity_check(device)

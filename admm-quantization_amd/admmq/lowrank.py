@@ -1,0 +1,184 @@
+"""Quant + low-rank ADMM on the MI355X (``scripts/factorize_lowrank.py``).
+
+W is split as W ≈ W_q + W_r, W_q on a ``bits``-bit grid and W_r of rank ``rank``, by
+alternating two ADMM solves (``:141-170``), each ``admm_iteration(H, U, W, H2, proj_func,
+rho, max_iter, eps)`` (``:85-101``) with the other part held fixed.
+
+* The updates around the projection run as two fused HIP streams (C-ABI
+  ``admmq_lowrank_pre`` / ``admmq_lowrank_post``, bit-exact float32 op order) and the
+  ``r < eps and s < eps`` break is tested on the device: iterations are queued without a
+  host round trip each (the reference syncs every iteration); the loop polls the flag
+  every ``poll`` iterations to stop queueing early.
+* The quantization projection is the HIP quantizer (``admmq.quantize_tensor``).
+* The rank projection is ``project_rank`` (exact truncated SVD, the reference's
+  semantics) or ``SubspaceProjector``: a warm-started block subspace iteration that
+  converges to the same truncation (top-``rank`` singular triplets) with a few thin
+  GEMMs per call instead of a full SVD of a 4096 x 11008 matrix.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import os
+import time
+from functools import partial
+from typing import Callable, List, Optional
+
+import torch
+
+from . import _lib
+from .quantization import quantize_tensor
+
+
+def project_rank(H: torch.Tensor, rank: int) -> torch.Tensor:
+    """``U[:, :rank] @ diag(S[:rank]) @ Vt[:rank]`` of ``torch.linalg.svd(H)`` (:80-82)."""
+    U, S, Vt = torch.linalg.svd(H, full_matrices=False)
+    return U[:, :rank] @ torch.diag(S[:rank]) @ Vt[:rank]
+
+
+class SubspaceProjector:
+    """Rank-``rank`` truncation by block subspace iteration, warm-started from the previous
+    call's subspace (consecutive ADMM iterates differ little). Each sweep runs
+    Q <- orth(X X^T Q) (thin GEMMs on the device) and the small SVD of Q^T X; it stops
+    when the top-``rank`` left singular subspace moves by less than ``tol``
+    (sin-theta distance sqrt(rank - ||U_prev^T U||_F^2)), then projects.
+    ``oversample`` extra columns speed up convergence of the last wanted triplet."""
+
+    def __init__(self, rank: int, oversample: int = 8, tol: float = 3e-6, max_sweeps: int = 100, seed: int = 0):
+        self.rank, self.k = rank, rank + oversample
+        self.tol, self.max_sweeps, self.seed = tol, max_sweeps, seed
+        self.Q: Optional[torch.Tensor] = None
+        self.sweeps: List[int] = []
+
+    def __call__(self, X: torch.Tensor) -> torch.Tensor:
+        m, n = X.shape
+        k = min(self.k, m, n)
+        r = min(self.rank, k)
+        if self.Q is None or self.Q.shape != (m, k):
+            g = torch.Generator().manual_seed(self.seed)
+            self.Q = torch.linalg.qr(X @ torch.randn(n, k, generator=g).to(X.device))[0]
+        Q = self.Q
+        Ur_prev = None
+        sweeps = 0
+        for sweeps in range(1, self.max_sweeps + 1):
+            Q = torch.linalg.qr(X @ (X.T @ Q))[0]
+            Ub, S, Vt = torch.linalg.svd(Q.T @ X, full_matrices=False)
+            Ur = Q @ Ub[:, :r]
+            if Ur_prev is not None:
+                c = float(torch.sum((Ur_prev.T @ Ur) ** 2))
+                if max(r - c, 0.0) ** 0.5 < self.tol:
+                    break
+            Ur_prev = Ur
+        self.Q = Q
+        self.sweeps.append(sweeps)
+        return Ur @ torch.diag(S[:r]) @ Vt[:r]
+
+
+def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.Tensor,
+                   proj_func: Callable[[torch.Tensor], torch.Tensor], rho: float = 1.0, max_iter: int = 50,
+                   eps: float = 1e-8, poll: int = 8, return_iters: bool = False):
+    """scripts/factorize_lowrank.py:85-101. Returns (H, U); U is updated in place and
+    returned (as in the reference); the caller's H is not written."""
+    for t in (H, U, W, H2):
+        _lib.require_device(t)
+    if not (H.shape == U.shape == W.shape == H2.shape):
+        raise ValueError("admmq.lowrank: H, U, W, H2 must have one shape")
+    lib = _lib.load()
+    dev = H.device
+    s = _lib.stream_handle(dev)
+    n = H.numel()
+    Hc = H.contiguous().clone()
+    Uc = U if U.is_contiguous() else U.contiguous()
+    Wc, H2c = W.contiguous(), H2.contiguous()
+    Hb, X = torch.empty_like(Hc), torch.empty_like(Hc)
+    ws = _lib.workspace(lib.admmq_lowrank_workspace_size(n), dev)
+    wsp, wsn = _lib.ptr(ws), ws.numel()
+    _lib.check(lib.admmq_lowrank_reset(wsp, wsn, s), "lowrank_reset")
+    for j in range(1, max_iter):
+        _lib.check(lib.admmq_lowrank_pre(_lib.ptr(Hc), _lib.ptr(Uc), _lib.ptr(Wc), _lib.ptr(H2c), _lib.ptr(Hb),
+                                         _lib.ptr(X), n, ctypes.c_float(rho), wsp, wsn, s), "lowrank_pre")
+        Hn = proj_func(X).contiguous()
+        if Hn.shape != Hc.shape or Hn.dtype != torch.float32 or Hn.device != dev:
+            raise ValueError("admmq.lowrank: proj_func must return a float32 tensor of X's shape on X's device")
+        _lib.check(lib.admmq_lowrank_post(_lib.ptr(Hn), _lib.ptr(Hb), _lib.ptr(Hc), _lib.ptr(Uc), n,
+                                          ctypes.c_float(eps), wsp, wsn, s), "lowrank_post")
+        if poll and j % poll == 0 and int(ws[:4].view(torch.int32)[0]):
+            break
+    if Uc is not U:
+        U.copy_(Uc)
+    iters = int(ws[:12].view(torch.int32)[2])
+    return (Hc, U, iters) if return_iters else (Hc, U)
+
+
+def factorize_lowrank(W: torch.Tensor, bits: int, rank: int, qscheme: str = "tensor_minmax", max_iter: int = 100,
+                      inner_iter: int = 50, rho: float = 1.0, seed: int = 42, projection: str = "svd",
+                      log_every: int = 10, logger=None):
+    """The alternating loop of scripts/factorize_lowrank.py:141-170 (init 'random').
+    Returns (W_q, W_r, rel_history). Random starts come from the CPU generator (seeded)."""
+    _lib.require_device(W)
+    dev = W.device
+    g = torch.Generator().manual_seed(seed)
+    quant = partial(quantize_tensor, qscheme=qscheme, bits=bits)
+    proj = partial(project_rank, rank=rank) if projection == "svd" else SubspaceProjector(rank, seed=seed)
+    W_q = torch.randn(*W.shape, generator=g).to(dev)
+    U_q = torch.zeros_like(W_q)
+    W_r = proj(torch.randn(*W.shape, generator=g).to(dev))
+    U_r = torch.zeros_like(W_r)
+    hist = []
+    nw = torch.linalg.norm(W)
+    for i in range(max_iter):
+        W_q, U_q = admm_iteration(W_q, U_q, W, W_r, quant, rho=rho, max_iter=inner_iter)
+        W_r, U_r = admm_iteration(W_r, U_r, W, W_q, proj, rho=rho, max_iter=inner_iter)
+        rel = float(torch.linalg.norm(W - W_r - W_q) / nw)
+        if logger and i % log_every == 0:
+            logger(f"Diff between W and (W_q + W_r) rel: {rel:.4f}")
+        if hist and hist[-1] < rel - 1:
+            hist.append(rel)
+            break
+        hist.append(rel)
+    return W_q, W_r, hist
+
+
+def main(argv=None):
+    """CLI of scripts/factorize_lowrank.py (same flags). Pretrained weights cannot be
+    downloaded here: ``--weights`` loads a state_dict (weights_only), else the layer is
+    a seeded synthetic Llama-7B weight of the same shape (admmq.synthetic)."""
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model-id", type=str, default="huggyllama/llama-7b")
+    ap.add_argument("--cache-dir", type=str, default=None)
+    ap.add_argument("--output-dir", type=str, default=".")
+    ap.add_argument("--with-wandb", action="store_true")
+    ap.add_argument("--layer", type=str, default="model.layers.0.self_attn.q_proj")
+    ap.add_argument("--max-iter", required=True, type=int)
+    ap.add_argument("--bits", required=True, type=int)
+    ap.add_argument("--rank", required=True, type=int)
+    ap.add_argument("--qscheme", type=str, default="tensor_minmax")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--weights", type=str, default=None)
+    ap.add_argument("--projection", choices=["svd", "subspace"], default="svd")
+    a = ap.parse_args(argv)
+    if not torch.cuda.is_available():
+        raise RuntimeError("admmq.lowrank needs a ROCm GPU")
+    dev = torch.device("cuda:0")
+    if a.weights:
+        W = torch.load(a.weights, map_location="cpu", weights_only=True)[f"{a.layer}.weight"].float()
+    else:
+        from . import synthetic
+        short = a.layer.split("layers.0.")[-1]
+        specs = {s.name: (i, s) for i, s in enumerate(synthetic.llama_layers())}
+        i, spec = specs.get(short, (0, synthetic.llama_layers()[0]))
+        W = torch.from_numpy(synthetic.layer_weight(spec, i))
+    W = W.to(dev)
+    t0 = time.time()
+    W_q, W_r, hist = factorize_lowrank(W, a.bits, a.rank, a.qscheme, a.max_iter, seed=a.seed,
+                                       projection=a.projection, logger=print)
+    print(f"done in {time.time() - t0:.1f}s, rel {hist[-1]:.4f}")
+    os.makedirs(a.output_dir, exist_ok=True)
+    rel = hist[-1]
+    torch.save(W_q.cpu(), os.path.join(a.output_dir, f'{a.layer}_{a.bits}_{a.rank}_{rel:.3f}_Q.pt'))
+    torch.save(W_r.cpu(), os.path.join(a.output_dir, f'{a.layer}_{a.bits}_{a.rank}_{rel:.3f}_R.pt'))
+    return W_q, W_r, hist
+
+
+if __name__ == "__main__":
+    main()

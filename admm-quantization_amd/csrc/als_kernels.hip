@@ -319,7 +319,6 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
   for (auto& a : pl.units)
     for (auto& b : a) b.clear();
   pl.split_ids.clear();
-  size_t part_floats = 0;
   int err_units = 0;
   for (int l = 0; l < n; ++l) {
     const admmq_cp_layer& L = layers[l];
@@ -351,7 +350,7 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
       j.nsplit = choose_split(tm * tn, j.K);
       j.kchunk = cdiv(cdiv(j.K, j.nsplit), kAlsBK) * kAlsBK;
       j.nsplit = cdiv(j.K, j.kchunk);
-      if (j.nsplit > 1) { pl.split_ids.push_back(l); part_floats += al((size_t)j.nsplit * j.M * j.N); }
+      if (j.nsplit > 1) pl.split_ids.push_back(l);
       for (int ks = 0; ks < j.nsplit; ++ks)
         for (int a = 0; a < tm; ++a)
           for (int b = 0; b < tn; ++b) pl.units[bi][0].push_back({l, a, b, ks});

@@ -1,0 +1,137 @@
+// Quant + low-rank ADMM (scripts/factorize_lowrank.py:85-101, admm_iteration):
+//
+//   for j in 1 .. max_iter-1:
+//     H_ = (rho (H + U) + W - H2) / (1 + rho)          k_lr_pre   (also X = H_ - U)
+//     H  = proj(H_ - U)                                 caller: quantizer or rank projection
+//     U += H - H_ ;  r = |H - H_|^2/|H|^2 ;  s = |H - H_prev|^2/|U|^2 ;  break if r, s < eps
+//                                                       k_lr_post  (H_prev is the old H)
+//
+// Both kernels are elementwise streams (HBM-bound: pre 20 B/element, post 20 B/element
+// + the projection's own pass); every float32 operation is in the reference's order.
+// The break test runs on the device: post's blocks write fp64 partial sums, the last
+// block to arrive sums them in block order (deterministic), tests r < eps and s < eps
+// and sets the sticky `done` word; later pre/post launches see it and do nothing, so
+// the caller queues all max_iter-1 iterations without a host round trip per iteration.
+#include <algorithm>
+#include <string>
+
+#include "../../include/admmq.h"
+#include "admmq_internal.h"
+
+namespace admmq {
+
+constexpr int kLrBlocks = 1024;   // fixed grid: partial sums have a fixed order
+constexpr int kLrThreads = 256;
+
+struct LrState {
+  int done, ticket, iters, pad_;
+};
+
+__global__ __launch_bounds__(kLrThreads) void k_lr_pre(const float* __restrict__ H, const float* __restrict__ U,
+                                                       const float* __restrict__ W, const float* __restrict__ H2,
+                                                       float* __restrict__ Hbar, float* __restrict__ X, long long n,
+                                                       float rho, float den, const LrState* __restrict__ st) {
+  if (st->done) return;
+  for (long long e = (long long)blockIdx.x * kLrThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kLrThreads) {
+    const float hu = H[e] + U[e];
+    const float t = ((rho * hu + W[e]) - H2[e]) / den;   // (rho*(H + U) + W - H2) / (1 + rho)
+    Hbar[e] = t;
+    X[e] = t - U[e];
+  }
+}
+
+__device__ __forceinline__ double lr_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(kLrThreads) void k_lr_post(const float* __restrict__ Hn, const float* __restrict__ Hbar,
+                                                        float* __restrict__ H, float* __restrict__ U, long long n,
+                                                        float eps, LrState* __restrict__ st, double* __restrict__ part) {
+  if (st->done) return;
+  // contiguous chunk per block: the block partials do not depend on the grid schedule
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long b0 = (long long)blockIdx.x * per, b1 = min(n, b0 + per);
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  for (long long e = b0 + threadIdx.x; e < b1; e += kLrThreads) {
+    const float hn = Hn[e], hb = Hbar[e], hp = H[e];
+    const float d = hn - hb;
+    const float u = U[e] + d;                    // U += H - H_
+    U[e] = u;
+    H[e] = hn;
+    const float dp = hn - hp;
+    s1 += (double)d * d;                         // sum (H - H_)^2
+    s2 += (double)hn * hn;                       // sum H^2
+    s3 += (double)dp * dp;                       // sum (H - H_prev)^2
+    s4 += (double)u * u;                         // sum U^2
+  }
+  __shared__ double red[4][kLrThreads / 64];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  s1 = lr_wave_sum(s1); s2 = lr_wave_sum(s2); s3 = lr_wave_sum(s3); s4 = lr_wave_sum(s4);
+  if (lane == 0) { red[0][w] = s1; red[1][w] = s2; red[2][w] = s3; red[3][w] = s4; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < kLrThreads / 64; ++q)
+      for (int k = 0; k < 4; ++k) t[k] += red[k][q];
+    double* mine = part + 4 * (size_t)blockIdx.x;
+    for (int k = 0; k < 4; ++k) __hip_atomic_store(mine + k, t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+    const int old = __hip_atomic_fetch_add(&st->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old + 1 == (int)gridDim.x;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  for (unsigned b = 0; b < gridDim.x; ++b)
+    for (int k = 0; k < 4; ++k) t[k] += __hip_atomic_load(part + 4 * (size_t)b + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  st->ticket = 0;
+  st->iters += 1;
+  if (t[0] / t[1] < (double)eps && t[2] / t[3] < (double)eps) st->done = 1;
+}
+
+static size_t lr_bytes() { return 256 + (size_t)kLrBlocks * 4 * sizeof(double); }
+
+static int lr_grid(long long n) { return (int)std::max(1LL, std::min<long long>(kLrBlocks, (n + kLrThreads - 1) / kLrThreads)); }
+
+}  // namespace admmq
+
+using namespace admmq;
+
+extern "C" {
+
+size_t admmq_lowrank_workspace_size(int64_t n) { return n < 0 ? 0 : lr_bytes(); }
+
+int32_t admmq_lowrank_reset(void* workspace, size_t workspace_bytes, void* stream) {
+  if (!workspace || workspace_bytes < lr_bytes()) return set_error(ADMMQ_ERR_WORKSPACE, "lowrank: workspace too small");
+  if (hipMemsetAsync(workspace, 0, sizeof(LrState), static_cast<hipStream_t>(stream)) != hipSuccess)
+    return set_error(ADMMQ_ERR_HIP, "lowrank: reset failed");
+  return ADMMQ_OK;
+}
+
+int32_t admmq_lowrank_pre(const float* H, const float* U, const float* W, const float* H2, float* Hbar, float* X,
+                          int64_t n, float rho, void* workspace, size_t workspace_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!H || !U || !W || !H2 || !Hbar || !X))) return set_error(ADMMQ_ERR_ARG, "lowrank_pre: bad arguments");
+  if (!workspace || workspace_bytes < lr_bytes()) return set_error(ADMMQ_ERR_WORKSPACE, "lowrank: workspace too small");
+  if (n == 0) return ADMMQ_OK;
+  const LrState* st = static_cast<const LrState*>(workspace);
+  hipLaunchKernelGGL(k_lr_pre, dim3(lr_grid(n)), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), H, U, W, H2,
+                     Hbar, X, (long long)n, rho, 1.0f + rho, st);
+  return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "lowrank_pre: launch failed");
+}
+
+int32_t admmq_lowrank_post(const float* Hn, const float* Hbar, float* H, float* U, int64_t n, float eps,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  if (n <= 0 || !Hn || !Hbar || !H || !U) return set_error(ADMMQ_ERR_ARG, "lowrank_post: bad arguments");
+  if (!workspace || workspace_bytes < lr_bytes()) return set_error(ADMMQ_ERR_WORKSPACE, "lowrank: workspace too small");
+  LrState* st = static_cast<LrState*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256);
+  hipLaunchKernelGGL(k_lr_post, dim3(lr_grid(n)), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), Hn, Hbar, H,
+                     U, (long long)n, eps, st, part);
+  return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "lowrank_post: launch failed");
+}
+
+}  // extern "C"

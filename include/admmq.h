@@ -17,6 +17,8 @@
  *                                           G = B.T @ B * (C.T @ C), F = torch.einsum('abc,cr,br->ar', W, C, B), ...
  *   admmq_cp_rel_error                   <- scripts/factorize.py:246-253 + source/admm.py:14-15
  *                                           squared_relative_diff(W, torch.einsum('ir,jr,kr->ijk', A, B, C))
+ *   admmq_lowrank_pre / _post            <- scripts/factorize_lowrank.py:85-101 admm_iteration(H,U,W,H2,proj_func,
+ *                                           rho,max_iter,eps): the updates around the projection, device break test
  */
 #ifndef ADMMQ_H_
 #define ADMMQ_H_
@@ -137,6 +139,20 @@ int32_t admmq_cp_gram_mttkrp(const admmq_cp_layer* layers, int32_t n, int32_t mo
  * materialising the reconstruction (fp32 MFMA products, fp64 sums). */
 int32_t admmq_cp_rel_error(const admmq_cp_layer* layers, int32_t n, double* out, void* workspace,
                            size_t workspace_bytes, void* stream);
+
+/* Quant + low-rank ADMM (scripts/factorize_lowrank.py:85-101), one iteration =
+ *   admmq_lowrank_pre   Hbar = (rho (H + U) + W - H2) / (1 + rho),  X = Hbar - U
+ *   (caller)            Hn = proj(X)   (quantizer: admmq_quantize_batched; or a rank projection)
+ *   admmq_lowrank_post  U += Hn - Hbar; H = Hn; residuals r, s; sticky done when r < eps and s < eps
+ * All buffers are n contiguous floats. The workspace holds {done, ticket, iterations, 0}
+ * (int32) at offset 0 and the fp64 partial sums; admmq_lowrank_reset zeroes the state
+ * before a call's first iteration. After `done`, pre/post do nothing. */
+size_t admmq_lowrank_workspace_size(int64_t n);
+int32_t admmq_lowrank_reset(void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_lowrank_pre(const float* H, const float* U, const float* W, const float* H2, float* Hbar, float* X,
+                          int64_t n, float rho, void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_lowrank_post(const float* Hn, const float* Hbar, float* H, float* U, int64_t n, float eps,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);

@@ -16,6 +16,8 @@ Fixture families:
   F3  short ALS loop  -> f3_als.npz
   F4  long-horizon objective band over torch thread counts -> f4_band.json
   F5  candidate grids (torch.linspace) -> f5_linspace.npz
+  F6  quant + low-rank ADMM (scripts/factorize_lowrank.py admm_iteration / project_rank)
+      -> f6_lowrank.npz  (the script is imported with ``bitsandbytes`` stubbed)
 """
 from __future__ import annotations
 
@@ -231,6 +233,52 @@ def gen_f4(ref_admm, ref_quant, out):
         json.dump(res, f, indent=1)
 
 
+def import_lowrank(path):
+    """scripts/factorize_lowrank.py as a module (its main() is guarded); bitsandbytes,
+    which it imports but never calls on this path, is stubbed."""
+    import importlib.util
+    sys.modules.setdefault("bitsandbytes", _Stub("bitsandbytes"))
+    spec = importlib.util.spec_from_file_location("ref_factorize_lowrank",
+                                                  os.path.join(path, "scripts", "factorize_lowrank.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def gen_f6(ref_quant, lowrank, out):
+    """One inner admm_iteration per projection at max_iter 2 / 3 / 50, then 3 outer
+    iterations of the alternating loop of scripts/factorize_lowrank.py:141-170."""
+    from functools import partial
+    arrays = {}
+    rng = np.random.default_rng(606)
+    W = torch.from_numpy((rng.standard_normal((96, 64)) * 0.05).astype(np.float32))
+    rank, bits = 4, 4
+    g = torch.Generator().manual_seed(42)
+    Wq0 = torch.randn(*W.shape, generator=g)
+    Wr0 = lowrank.project_rank(torch.randn(*W.shape, generator=g), rank)
+    arrays.update(W=W.numpy(), Wq0=Wq0.numpy(), Wr0=Wr0.numpy())
+    for qs in ("tensor_minmax", "tensor_mseminmax_symmetric"):
+        qf = partial(ref_quant.quantize_tensor, qscheme=qs, bits=bits)
+        pf = partial(lowrank.project_rank, rank=rank)
+        for mi in (2, 3, 50):
+            H, U = lowrank.admm_iteration(Wq0.clone(), torch.zeros_like(Wq0), W, Wr0, qf, rho=1.0, max_iter=mi)
+            arrays[f"{qs}_q_it{mi}_H"], arrays[f"{qs}_q_it{mi}_U"] = H.numpy(), U.numpy()
+        for mi in (2, 3):
+            H, U = lowrank.admm_iteration(Wr0.clone(), torch.zeros_like(Wr0), W, Wq0, pf, rho=1.0, max_iter=mi)
+            arrays[f"r_it{mi}_H"], arrays[f"r_it{mi}_U"] = H.numpy(), U.numpy()
+        Wq, Uq, Wr, Ur = Wq0.clone(), torch.zeros_like(Wq0), Wr0.clone(), torch.zeros_like(Wr0)
+        rel = []
+        for _ in range(3):
+            Wq, Uq = lowrank.admm_iteration(Wq, Uq, W, Wr, qf, rho=1.0)
+            Wr, Ur = lowrank.admm_iteration(Wr, Ur, W, Wq, pf, rho=1.0)
+            rel.append(float(torch.linalg.norm(W - Wr - Wq) / torch.linalg.norm(W)))
+        arrays[f"{qs}_outer_Wq"], arrays[f"{qs}_outer_Wr"] = Wq.numpy(), Wr.numpy()
+        arrays[f"{qs}_outer_Uq"], arrays[f"{qs}_outer_Ur"] = Uq.numpy(), Ur.numpy()
+        arrays[f"{qs}_outer_rel"] = np.array(rel)
+    np.savez_compressed(os.path.join(out, "f6_lowrank.npz"), **arrays)
+    print("F6:", len(arrays), "arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -239,7 +287,7 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(8)
     ref_admm, ref_quant = import_reference(a.reference)
-    only = set(a.only.split(",")) if a.only else {"f1", "f2", "f3", "f4", "f5"}
+    only = set(a.only.split(",")) if a.only else {"f1", "f2", "f3", "f4", "f5", "f6"}
     if "f5" in only:
         gen_f5(HERE)
     if "f1" in only:
@@ -248,6 +296,8 @@ def main():
         gen_f2(ref_admm, HERE)
     if "f3" in only:
         gen_f3(ref_admm, ref_quant, HERE)
+    if "f6" in only:
+        gen_f6(ref_quant, import_lowrank(a.reference), HERE)
     if "f4" in only and not a.skip_band:
         gen_f4(ref_admm, ref_quant, HERE)
     meta = {"torch": torch.__version__, "numpy": np.__version__, "threads": 8,

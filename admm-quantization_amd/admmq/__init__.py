@@ -7,6 +7,9 @@ Drop-in replacements for KamikaziZen/admm-quantization's hot path:
     source.utils.unfold                                                 -> admmq.utils
     source.parafac_epc.parafac_epc                                      -> admmq.parafac_epc
     scripts/factorize.py (ALS driver + CLI)                             -> admmq.factorize
+      (Gram∘Gram / MTTKRP / reconstruction error on the device)         -> admmq.als
+    scripts/factorize_lowrank.py (quant + low-rank ADMM + CLI)          -> admmq.lowrank
+    source.models.build_cp_layer / build_cp2conv_layer / ... (export)   -> admmq.export
 
 Compute runs in libadmmq.so (hand-written HIP for gfx950) through a C ABI
 (include/admmq.h); there is no CPU fallback.

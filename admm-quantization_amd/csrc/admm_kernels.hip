@@ -70,11 +70,10 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
                                                        int ncand, int bits, int scheme, int slot, int iter) {
   const Chunk ck = chunks[blockIdx.x];
   const ProbDesc& p = probs[ck.job];
-  if (p.flags[0]) return;
   const long long total = (long long)p.I * p.ld;
   // float4 group g of thread t at start + 4 t + 1024 g. Element loads first: independent
-  // of the quantizer parameters, so their latency overlaps the parameter chain
-  // (stat -> sel -> sse) below.
+  // of the quantizer parameters and of the stop flag, so their latency overlaps the
+  // parameter chain (stat -> sel -> sse) and the flag read below.
   float4 x4[G], t4[G], h4[G], u4[G], f4[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -88,6 +87,7 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
       f4[g] = *reinterpret_cast<const float4*>(p.Fp + e);
     }
   }
+  if (p.flags[0]) return;   // converged earlier (sticky break)
   const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);
   const float rho = p.rho[0];
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;

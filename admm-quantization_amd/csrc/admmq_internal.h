@@ -92,7 +92,16 @@ struct QJob {
 struct GemmTile { int prob, tm, tn, first, k0, nk, part, ks; };
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
 struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
-struct Chunk { int job, start; };
+// Work unit {job, first element}. Stage-1 units also carry the job's inputs that the
+// kernel's first loads need (the search state, the stop flag, the tensor and its size),
+// so those loads do not wait on a dependent descriptor read.
+struct Chunk {
+  int job, start;
+  const unsigned* stat;
+  const int* done;
+  const float* X;
+  long long total;
+};
 
 // float <-> order-preserving unsigned encodings for atomicMin/Max
 __device__ __forceinline__ unsigned enc_ord(float f) {

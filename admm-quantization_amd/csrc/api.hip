@@ -362,7 +362,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     const long long tot = (long long)d.I * d.ld;
     for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
     const long long hu = (long long)kHistElems * pl.hist_nv;
-    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e});
+    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.X, tot});
     pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
   }
   pl.d_desc = cv.take<ProbDesc>(nprob);
@@ -446,7 +446,7 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
     const long long tot = (long long)j.rows * j.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
     for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
-    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e});
+    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e, j.mv.stat, nullptr, j.Xp, tot});
     pl.jobs[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
   pl.d_jobs = cv.take<QJob>(n);

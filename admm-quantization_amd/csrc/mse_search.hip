@@ -128,11 +128,11 @@ __global__ void k_check_thresholds(unsigned seed, int nsamp, unsigned* mismatche
 int check_thresholds(unsigned seed, int nsamp) {
   unsigned* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return -1;
-  hipMemset(d, 0, sizeof(unsigned));
+  (void)hipMemset(d, 0, sizeof(unsigned));
   hipLaunchKernelGGL(k_check_thresholds, dim3(256), dim3(256), 0, 0, seed, nsamp, d);
   unsigned h = 0;
   const bool ok = hipMemcpy(&h, d, sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess;
-  hipFree(d);
+  (void)hipFree(d);
   return ok ? (int)h : -1;
 }
 
@@ -558,10 +558,21 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
                                                       const unsigned short* __restrict__ groups, int ngroups) {
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   const Chunk ck = chunks[blockIdx.x];
+  // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
+  // this thread's elements; the descriptor fields are read alongside
+  const int stopped = ck.done ? *ck.done : 0;
+  const float mx = __uint_as_float(ck.stat[4 * slot]);
+  const long long total = ck.total;
+  float4 x4[2 * NV];
+#pragma unroll
+  for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x4[hh] = *reinterpret_cast<const float4*>(ck.X + e);
+  }
   const MseView& v = mview(d, qj, ck.job);
-  if (v.done && *v.done) return;
+  if (stopped) return;
   int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-  const float mx = __uint_as_float(v.stat[4 * slot]);
   if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
     if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
     return;
@@ -582,14 +593,6 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
   __shared__ unsigned long long wtot[8], wtot2[8];
   __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
-  const long long total = (long long)v.rows * v.ld;
-  float4 x4[2 * NV];
-#pragma unroll
-  for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
-    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4[hh] = *reinterpret_cast<const float4*>(v.X + e);
-  }
   fill_thresholds(thr, mx, n, QMAX);
   for (int i = threadIdx.x; i < M; i += blockDim.x) rnk[i] = rank0[i];
   for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }

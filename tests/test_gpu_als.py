@@ -171,3 +171,18 @@ def test_bad_arguments_raise(torch_dev):
         gram_mttkrp(W, [torch.zeros(4, 3, device=dev), torch.zeros(5, 3, device=dev), torch.zeros(6, 2, device=dev)], 0)
     with pytest.raises(RuntimeError):
         gram_mttkrp(W.cpu(), [torch.zeros(n, 3) for n in (4, 5, 6)], 0)
+
+
+def test_init_parafac_epc_on_device(torch_dev):
+    """init_factors(init='parafac-epc') (source/admm.py:40-44: 50 ALS + 50 EPC iterations)
+    runs on the device and hands float32 factors of the layer's shapes to the ADMM driver;
+    objective only (parity unpinned: tensorly / musco absent)."""
+    torch, dev = torch_dev
+    from admmq import init_factors, synthetic
+    from admmq.parafac_epc import _reconstruct
+    idx, spec = synthetic.find_layer("resnet18", "layer1.0.conv1")
+    W = _t(torch, dev, synthetic.layer_weight(spec, idx))
+    fs = init_factors(W, spec.rank(), init="parafac-epc", device=dev, seed=42)
+    assert [tuple(f.shape) for f in fs] == [(64, spec.rank()), (64, spec.rank()), (9, spec.rank())]
+    assert all(f.dtype == torch.float32 and f.device.type == "cuda" for f in fs)
+    assert all(bool(torch.isfinite(f).all()) for f in fs)

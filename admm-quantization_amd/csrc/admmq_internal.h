@@ -125,6 +125,7 @@ void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
                  float* kpart, unsigned* pcnt, int slot, int iter, float eps, int ncand, hipStream_t s);
 int gemm_split_min_steps();
+int gemm_persistent_per_cu();
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);

@@ -57,6 +57,8 @@ struct Prof {
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
+// Big GEMM tiles dealt to CUs by K-steps (ADMMQ_GEMM_CUBAL=0: longest-first order only).
+static bool g_cu_balance = !getenv("ADMMQ_GEMM_CUBAL") || atoi(getenv("ADMMQ_GEMM_CUBAL")) != 0;
 // Big GEMM tiles placed by whole layers per XCD (ADMMQ_GEMM_XCD=1; default: the column-interleaved order).
 static bool g_xcd_layers = getenv("ADMMQ_GEMM_XCD") && atoi(getenv("ADMMQ_GEMM_XCD")) != 0;
 // Stage-1 form: merged thresholds (k_mse_hist3, default where supported) or per-level
@@ -168,6 +170,34 @@ static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
   GemmTile t;
   t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.k0 = 0; t.nk = nk; t.part = -1; t.ks = 0;
   return t;
+}
+
+// CU-balanced order of the big GEMM tiles. When every tile of a launch is resident at
+// once (at most `slots` workgroups per CU), workgroup b lands on CU b mod ncu (round
+// robin over the XCDs, then over each XCD's CUs; tools/gemm_timeline.py checks it), so
+// the tiles at positions b, b + ncu, b + 2 ncu share one CU's MFMA pipes. Longest-first
+// order alone gives some CUs three long tiles and others two; instead every tile, longest
+// first, goes to the CU with the fewest K-steps that still has a free slot.
+static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots) {
+  const int n = (int)tiles.size();
+  if (n <= ncu || n > ncu * slots) return;
+  const int rounds = (n + ncu - 1) / ncu;
+  const int full = n - (rounds - 1) * ncu;   // CUs 0 .. full-1 take `rounds` tiles, the rest one fewer
+  std::vector<GemmTile> sorted = tiles;
+  std::stable_sort(sorted.begin(), sorted.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
+  std::vector<std::vector<GemmTile>> bins(ncu);
+  std::vector<long long> load(ncu, 0);
+  for (const GemmTile& t : sorted) {
+    int best = -1;
+    for (int b = 0; b < ncu; ++b) {
+      const int cap = b < full ? rounds : rounds - 1;
+      if ((int)bins[b].size() < cap && (best < 0 || load[b] < load[best])) best = b;
+    }
+    bins[best].push_back(t);
+    load[best] += t.nk;
+  }
+  for (int b = 0; b < ncu; ++b)
+    for (int r = 0; r < (int)bins[b].size(); ++r) tiles[b + (size_t)r * ncu] = bins[b][r];
 }
 
 // Whole-layer XCD placement of the big GEMM tiles. Workgroup b runs on XCD b % 8
@@ -324,6 +354,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     std::stable_sort(out.begin(), out.end(), [](const GemmTile& x, const GemmTile& y) { return x.nk > y.nk; });
     pl.tiles.swap(out);
   }
+  if (g_cu_balance && pl.nsplit == 0 && gemm_persistent_per_cu() == 0) order_tiles_for_cus(pl.tiles, 256, 3);
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
     if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip != 32) continue;

@@ -143,12 +143,35 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
     const unsigned long long t_tile = __builtin_amdgcn_s_memrealtime();
     const GemmTile tl = tiles[t];
     const ProbDesc& p = probs[tl.prob];
+    const int ld = p.ld, ldm = p.ldm;
+    const int row0 = tl.tm * BM, col0 = tl.tn * BN;
+    const int nk = tl.nk;
+    // per-lane global source of each of this wave's glds pieces (K-step 0)
+    const float* src[GPW];
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      const int g = wave * GPW + j;
+      const int r = 8 * g + (lane >> 3);                       // image row
+      const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+      src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
+                        : p.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
+    }
+#define ADMMQ_ISSUE(s, kt)                                                 \
+  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
+    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
+    // the first NS-1 stages go out before the stop test, whose inputs (flag, residual
+    // sums) are one dependent read further away; a stopped problem drains them unused
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
     bool skip = p.flags[0] != 0;
     if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
       if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
       skip = true;
     }
-    if (skip && tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+    if (skip) {
+      wait_vmcnt<0>();   // the speculative stage loads land before the LDS is reused or the wave ends
+      if (tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
+    }
     if (!skip) {
       if (tl.first && tl.ks == 0) {   // this iteration's quantizer-search accumulators start at zero
         unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
@@ -158,23 +181,6 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
         for (int c = tid; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
         if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
       }
-      const int ld = p.ld, ldm = p.ldm;
-      const int row0 = tl.tm * BM, col0 = tl.tn * BN;
-      const int nk = tl.nk;
-
-      // per-lane global source of each of this wave's glds pieces (K-step 0)
-      const float* src[GPW];
-#pragma unroll
-      for (int j = 0; j < GPW; ++j) {
-        const int g = wave * GPW + j;
-        const int r = 8 * g + (lane >> 3);                       // image row
-        const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
-        src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
-                          : p.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
-      }
-#define ADMMQ_ISSUE(s, kt)                                                 \
-  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
-    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
 
       f32x16 acc;
 #pragma unroll
@@ -204,8 +210,6 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);               \
     }                                                                                   \
   } while (0)
-#pragma unroll
-      for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
       const int nfull = nk / NS * NS;
       for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
 #pragma unroll
@@ -570,6 +574,13 @@ int gemm_big_wm() {
 // Workgroups per CU for the persistent grid (MI355X: 256 CUs)
 static int gemm_grid(int ntiles, int per_cu) { return std::min(ntiles, 256 * per_cu); }
 
+// Persistent GEMM grid: workgroups per CU drawing tiles from the ticket queue (0: one
+// workgroup per tile).
+int gemm_persistent_per_cu() {
+  static const int v = env_int("ADMMQ_GEMM_PER_CU", 0);
+  return v;
+}
+
 // Tiles with at least this many K-steps are split into two K halves (0: never).
 int gemm_split_min_steps() {
   static const int v = env_int("ADMMQ_GEMM_SPLIT", 0);
@@ -582,7 +593,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
   // queue[0] / queue[1] are their ticket counters.
   static const int cfg_big = env_int("ADMMQ_GEMM_BIG", 13);     // KS*10 + NS
   static const int cfg_small = env_int("ADMMQ_GEMM_SMALL", 24);
-  static const int per_cu = env_int("ADMMQ_GEMM_PER_CU", 0);    // 0: one workgroup per tile
+  const int per_cu = gemm_persistent_per_cu();                    // 0: one workgroup per tile
 #define ADMMQ_GEMM(WM, KS, NS, n, t, q)                                                                      \
   hipLaunchKernelGGL((k_gemm<WM, KS, NS>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, d, \
                      t, n, q, kpart, pcnt, slot, iter, eps, ncand)

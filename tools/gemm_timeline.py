@@ -71,3 +71,9 @@ for r in recs:
     per_cu[(r[3], r[4], r[5], r[6])].add(r[7])
 cnt = collections.Counter(len(v) for v in per_cu.values())
 print("workgroups per CU histogram:", dict(sorted(cnt.items())), "CUs", len(per_cu))
+# placement check for the CU-balanced tile order: do workgroups b and b + 256 share a CU?
+where = {r[7]: (r[3], r[4], r[5], r[6]) for r in recs}
+pairs = [(b, b + 256) for b in range(len(recs)) if b + 256 in where and b in where]
+same = sum(1 for a, b in pairs if where[a] == where[b])
+print(f"placement: workgroups b and b+256 on the same CU for {same}/{len(pairs)} pairs; "
+      f"same XCD for {sum(1 for a, b in pairs if where[a][0] == where[b][0])}/{len(pairs)}")

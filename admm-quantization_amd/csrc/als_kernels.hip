@@ -37,6 +37,7 @@ struct AlsJob {
   int M, N, K;         // output rows / cols, reduction length
   int nsplit, kchunk;  // MTTKRP: K chunks and their length (multiple of kAlsBK)
   int K2, afast;       // MTTKRP: Khatri-Rao inner extent; 1 = W_(n) rows are the contiguous index
+  float invK2;         // 1 / K2 (fast exact div/mod)
   int R, Kx;           // Gram: R, rows of Y (0: 2-way, no Hadamard factor)
   long long sm, s1, s2;
   const float* W;      // MTTKRP / error: the layer tensor
@@ -51,6 +52,16 @@ struct AlsJob {
 };
 struct AlsUnit { int job, tm, tn, ks; };
 
+// q = k / d, r = k % d for 0 <= k < 2^24 and d >= 1 by a float reciprocal estimate and
+// one correction step each way (exact: k * (1/d) is within one of the true quotient).
+__device__ __forceinline__ int divmod(int k, int d, float inv, int& r) {
+  int q = (int)((float)k * inv);
+  r = k - q * d;
+  if (r < 0) { q -= 1; r += d; }
+  if (r >= d) { q += 1; r -= d; }
+  return q;
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 a;
 #pragma unroll
@@ -62,7 +73,8 @@ __device__ __forceinline__ f32x16 zero16() {
 // Callers guarantee the indices are in range.
 __device__ __forceinline__ float opA(const AlsJob& j, int kind, int m, int k, int which) {
   if (kind == 0) {
-    const int kq = j.K2 == 1 ? k : k / j.K2, kr = j.K2 == 1 ? 0 : k - kq * j.K2;
+    int kr = 0;
+    const int kq = j.K2 == 1 ? k : divmod(k, j.K2, j.invK2, kr);
     return j.W[(long long)m * j.sm + (long long)kq * j.s1 + (long long)kr * j.s2];
   }
   if (kind == 1) return (which ? j.Y : j.X)[(long long)k * j.R + m];   // X^T: A(m=r1, k=i) = X[i, r1]
@@ -71,13 +83,15 @@ __device__ __forceinline__ float opA(const AlsJob& j, int kind, int m, int k, in
 __device__ __forceinline__ float opB(const AlsJob& j, int kind, int k, int n, int which) {
   if (kind == 0) {
     if (!j.Y) return j.X[(long long)k * j.N + n];
-    const int kq = k / j.K2, kr = k - kq * j.K2;
+    int kr;
+    const int kq = divmod(k, j.K2, j.invK2, kr);
     return j.X[(long long)kq * j.N + n] * j.Y[(long long)kr * j.N + n];
   }
   if (kind == 1) return (which ? j.Y : j.X)[(long long)k * j.R + n];
   // error: B(k=r, n) = B[n / Kc, r] * C[n % Kc, r]   (Kc = K2 here)
   if (!j.Z) return j.Y[(long long)n * j.R + k];
-  const int nq = n / j.K2, nr = n - nq * j.K2;
+  int nr;
+  const int nq = divmod(n, j.K2, j.invK2, nr);
   return j.Y[(long long)nq * j.R + k] * j.Z[(long long)nr * j.R + k];
 }
 
@@ -375,6 +389,11 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
       for (int a = 0; a < cdiv(I, BM); ++a)
         for (int b = 0; b < cdiv(j.N, kAlsBN); ++b) pl.units[bi][2].push_back({l, a, b, 0});
       j.nunits = (int)pl.units[bi][2].size() - j.unit0;
+    }
+    j.invK2 = 1.0f / (float)std::max(j.K2, 1);
+    if (j.K2 > 1 && (kind == 0 ? j.K : j.N) >= (1 << 24)) {   // divmod's exact range
+      err = "cp layer " + std::to_string(l) + ": Khatri-Rao index range >= 2^24";
+      return ADMMQ_ERR_ARG;
     }
     pl.jobs.push_back(j);
   }

@@ -1,7 +1,7 @@
 """Quant + low-rank ADMM on the MI355X (``scripts/factorize_lowrank.py``).
 
 W is split as W ≈ W_q + W_r, W_q on a ``bits``-bit grid and W_r of rank ``rank``, by
-alternating two ADMM solves (``:141-170``), each ``admm_iteration(H, U, W, H2, proj_func,
+alternating two ADMM solves (``:156-170``), each ``admm_iteration(H, U, W, H2, proj_func,
 rho, max_iter, eps)`` (``:85-101``) with the other part held fixed.
 
 * The updates around the projection run as two fused HIP streams (C-ABI
@@ -113,7 +113,7 @@ def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.
 def factorize_lowrank(W: torch.Tensor, bits: int, rank: int, qscheme: str = "tensor_minmax", max_iter: int = 100,
                       inner_iter: int = 50, rho: float = 1.0, seed: int = 42, projection: str = "svd",
                       log_every: int = 10, logger=None):
-    """The alternating loop of scripts/factorize_lowrank.py:141-170 (init 'random').
+    """The alternating loop of scripts/factorize_lowrank.py:156-170 (init 'random').
     Returns (W_q, W_r, rel_history). Random starts come from the CPU generator (seeded)."""
     _lib.require_device(W)
     dev = W.device

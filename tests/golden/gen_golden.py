@@ -247,7 +247,7 @@ def import_lowrank(path):
 
 def gen_f6(ref_quant, lowrank, out):
     """One inner admm_iteration per projection at max_iter 2 / 3 / 50, then 3 outer
-    iterations of the alternating loop of scripts/factorize_lowrank.py:141-170."""
+    iterations of the alternating loop of scripts/factorize_lowrank.py:156-170."""
     from functools import partial
     arrays = {}
     rng = np.random.default_rng(606)

@@ -3,7 +3,7 @@
 //   k_rho        rho = trace(G)/R                       (admm.py:53; trace accumulated in fp64 like torch-CPU)
 //   k_pack       padded Fp/H/U copies, P = F + rho(H+U)  (admm.py:56, first iteration's right-hand side)
 //   k_fill_a64   A = G + rho I in fp64 for the SPD inverse (admm.py:54)
-//   k_finalize   H = Q(X) with the chosen scale, U += H - H_T, next P = F + rho(H+U),
+//   k_finalize   H = Q(X), X = H_T - U re-formed here, with the chosen scale, U += H - H_T, next P = F + rho(H+U),
 //                residual sums for the r/s stop test  (admm.py:59-65)
 //   k_unpack     padded H/U -> caller tensors
 #include "quant_device.h"
@@ -74,13 +74,12 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
   // float4 group g of thread t at start + 4 t + 1024 g. Element loads first: independent
   // of the quantizer parameters and of the stop flag, so their latency overlaps the
   // parameter chain (stat -> sel -> sse) and the flag read below.
-  float4 x4[G], t4[G], h4[G], u4[G], f4[G];
+  float4 t4[G], h4[G], u4[G], f4[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
-    x4[g] = make_float4(0.f, 0.f, 0.f, 0.f); t4[g] = x4[g]; h4[g] = x4[g]; u4[g] = x4[g]; f4[g] = x4[g];
+    t4[g] = make_float4(0.f, 0.f, 0.f, 0.f); h4[g] = t4[g]; u4[g] = t4[g]; f4[g] = t4[g];
     if (e < total) {
-      x4[g] = *reinterpret_cast<const float4*>(p.X + e);
       t4[g] = *reinterpret_cast<const float4*>(p.HT + e);
       h4[g] = *reinterpret_cast<const float4*>(p.H + e);
       u4[g] = *reinterpret_cast<const float4*>(p.U + e);
@@ -97,8 +96,9 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
     if (e >= total) continue;
     const int row = (int)(e / p.ld);
     const int c0 = (int)(e - (long long)row * p.ld);
-    const float xs[4] = {x4[g].x, x4[g].y, x4[g].z, x4[g].w}, ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
+    const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
     const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
+    const float xs[4] = {ts[0] - us[0], ts[1] - us[1], ts[2] - us[2], ts[3] - us[3]};   // H_T - U
     const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
     float ho[4], uo[4], po[4];
 #pragma unroll

@@ -37,7 +37,8 @@ constexpr int kThinK = 128;        // ... reduction rows per unit (4 waves x 32)
 // turns them into A(c) +- E(c) and the candidate set S; stage 2 evaluates the
 // canonical SSE only on S (sel = {nS, c*, list...}); nS == ncand means exhaustive.
 struct MseView {
-  const float* X;              // rows x ld, zero pads
+  const float* X;              // rows x ld, zero pads (ADMM: H_T, see U)
+  const float* U;              // non-null (ADMM): the quantizer input is X - U = H_T - U
   int rows, cols, ld, qpr;     // qpr = ceil(cols/4)
   int nq, nelem;               // quads of the valid region, rows*cols
   unsigned* stat;              // [slot][4] {absmax bits, min enc, max enc, 0}
@@ -100,8 +101,20 @@ struct Chunk {
   const unsigned* stat;
   const int* done;
   const float* X;
+  const float* U;   // non-null: the element is X - U (ADMM: H_T - U)
   long long total;
 };
+
+// Quantizer input elements at off..off+3: X, or H_T - U for an ADMM view (the GEMM
+// does not store X = H_T - U; every reader forms it with the same float32 subtraction).
+__device__ __forceinline__ float4 load_x4(const float* X, const float* U, long long off) {
+  float4 x = *reinterpret_cast<const float4*>(X + off);
+  if (U) {
+    const float4 u = *reinterpret_cast<const float4*>(U + off);
+    x.x -= u.x; x.y -= u.y; x.z -= u.z; x.w -= u.w;
+  }
+  return x;
+}
 
 // float <-> order-preserving unsigned encodings for atomicMin/Max
 __device__ __forceinline__ unsigned enc_ord(float f) {

@@ -301,7 +301,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.flags = cv.take<int>(4);
     d.rho = cv.take<float>(4);
     carve_view(cv, d.mv, 2, ncand);
-    d.mv.X = d.X; d.mv.rows = d.I; d.mv.cols = d.R; d.mv.ld = d.ld; d.mv.qpr = (d.R + 3) / 4;
+    d.mv.X = d.HT; d.mv.U = d.U; d.mv.rows = d.I; d.mv.cols = d.R; d.mv.ld = d.ld; d.mv.qpr = (d.R + 3) / 4;
     d.mv.nq = d.nq; d.mv.nelem = d.I * d.R; d.mv.done = d.flags;
     pl.maxIp = std::max(pl.maxIp, d.Ip); pl.maxld = std::max(pl.maxld, d.ld);
     pl.maxldm = std::max(pl.maxldm, d.ldm); pl.maxnbk = std::max(pl.maxnbk, d.nbk);
@@ -393,7 +393,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     const long long tot = (long long)d.I * d.ld;
     for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
     const long long hu = (long long)kHistElems * pl.hist_nv;
-    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.X, tot});
+    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
     pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
   }
   pl.d_desc = cv.take<ProbDesc>(nprob);
@@ -477,7 +477,7 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
     const long long tot = (long long)j.rows * j.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
     for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
-    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e, j.mv.stat, nullptr, j.Xp, tot});
+    for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e, j.mv.stat, nullptr, j.Xp, nullptr, tot});
     pl.jobs[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
   pl.d_jobs = cv.take<QJob>(n);

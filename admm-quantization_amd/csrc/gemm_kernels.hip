@@ -280,7 +280,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
             const float ht = acc[r];
             const float x = ht - p.U[off];
             p.HT[off] = ht;
-            p.X[off] = x;
+            if (p.X_dbg) p.X[off] = x;   // X = H_T - U is re-formed by its readers; stored for debug output only
             if (row < p.I && col < p.R) {
               amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
               const unsigned e = enc_ord(x);
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
       if (cok && row < I) {
         const size_t off = (size_t)row * ld + col;
         *(gst4*)(p.HT + off) = h4;
-        *(gst4*)(p.X + off) = x4;
+        if (p.X_dbg) *(gst4*)(p.X + off) = x4;
       }
     }
   }

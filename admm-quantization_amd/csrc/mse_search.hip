@@ -253,7 +253,7 @@ __device__ void sse_in_block(const MseView& v, const int* lsel, int ncand, int b
       const int qi = q0 + t;
       const int row = qi / v.qpr;
       const int qc = qi - row * v.qpr;
-      xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+      xs[t] = load_x4(v.X, v.U, (long long)row * v.ld + 4 * qc);
     }
     __syncthreads();
     sse_sweep_list(xs, nqc, mx, K, ncand, bits, all ? nullptr : lsel + 2, all ? ncand : ns,
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   for (int g = 0; g < NV; ++g) {
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 4096LL * g;
     x4v[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4v[g] = *reinterpret_cast<const float4*>(v.X + e);
+    if (e < total) x4v[g] = load_x4(v.X, v.U, e);
   }
   fill_thresholds(thr, mx, n, QMAX);
   if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
   for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
     x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4[hh] = *reinterpret_cast<const float4*>(ck.X + e);
+    if (e < total) x4[hh] = load_x4(ck.X, ck.U, e);
   }
   const MseView& v = mview(d, qj, ck.job);
   if (stopped) return;
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(256) void k_mse_sse(const ProbDesc* __restrict__ d,
         const int qi = ck.start + t;
         const int row = qi / v.qpr;
         const int qc = qi - row * v.qpr;
-        xs[t] = *reinterpret_cast<const float4*>(v.X + (size_t)row * v.ld + 4 * qc);
+        xs[t] = load_x4(v.X, v.U, (long long)row * v.ld + 4 * qc);
       }
       const bool all = ns >= ncand;
       if (!all)

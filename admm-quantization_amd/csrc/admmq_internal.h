@@ -143,6 +143,7 @@ int gemm_persistent_per_cu();
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
+size_t hist3_lds_bytes(int ncand, int bits);
 int copy_thin_trace(unsigned long long* host, int n);
 int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
@@ -152,6 +153,10 @@ int check_thresholds(unsigned seed, int nsamp);
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s);
+int small_admm_groups(long long maxtotal);
+void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ngr, int ncand, int bits, int slot,
+                           int iter, const unsigned short* rank0, const unsigned short* groups, int ngroups,
+                           hipStream_t s);
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);

@@ -57,6 +57,9 @@ struct Prof {
 static Prof g_prof;
 // A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
 static bool g_exhaustive = false;
+// Small jobs (I <= kThinRows) run stage 1, selection, stage 2 and finalize in one block
+// each (ADMMQ_SMALL_FUSED=0: the multi-block stage 1 + finalize launches instead).
+static bool g_small_fused = !getenv("ADMMQ_SMALL_FUSED") || atoi(getenv("ADMMQ_SMALL_FUSED")) != 0;
 // Big GEMM tiles dealt to CUs by K-steps (ADMMQ_GEMM_CUBAL=0: longest-first order only).
 static bool g_cu_balance = !getenv("ADMMQ_GEMM_CUBAL") || atoi(getenv("ADMMQ_GEMM_CUBAL")) != 0;
 // Big GEMM tiles placed by whole layers per XCD (ADMMQ_GEMM_XCD=1; default: the column-interleaved order).
@@ -157,6 +160,10 @@ struct AdmmPlan {
   int ntiles_big = 0, ntiles_small = 0;
   int fin_elems = kElemChunk;
   int hist_nv = 1;
+  std::vector<int> small;         // jobs with I <= kThinRows (one-block fused search + finalize)
+  int* d_small = nullptr;
+  int nfin_big = 0, nhist_big = 0;   // finalize / stage-1 units of the other jobs (listed first)
+  int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
 };
 
 // Thin factors (I <= kThinRows) take the VALU split-K solve (k_gemm_thin) unless
@@ -387,20 +394,32 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   }
   pl.fin_elems = big_units >= kFinMinUnits ? kFinElems : kElemChunk;
   pl.hist_nv = hist_units > kHistMaxUnits ? 2 : 1;   // one round of resident stage-1 blocks
-  for (int i : order) {
-    const ProbDesc& d = pl.desc[i];
-    for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
-    const long long tot = (long long)d.I * d.ld;
-    for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
-    const long long hu = (long long)kHistElems * pl.hist_nv;
-    for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
-    pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
+  // stage-1 / finalize units of the small jobs (I <= kThinRows) go last: when their
+  // fused one-block path runs (k_mse_small_admm), the launches take only the others
+  pl.small.clear();
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if ((d.I <= kThinRows) != (pass == 1)) continue;
+      if (pass == 1) pl.small.push_back(i);
+      for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
+      const long long tot = (long long)d.I * d.ld;
+      for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
+      const long long hu = (long long)kHistElems * pl.hist_nv;
+      for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
+      pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
+    }
+    if (pass == 0) { pl.nfin_big = (int)pl.fin_chunks.size(); pl.nhist_big = (int)pl.hist_chunks.size(); }
   }
+  long long small_max = 0;
+  for (int i : pl.small) small_max = std::max(small_max, (long long)pl.desc[i].I * pl.desc[i].ld);
+  pl.small_groups = small_admm_groups(small_max);
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
+  pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
   pl.d_queue = cv.take<unsigned>(2);
   pl.d_kpart = cv.take<float>((size_t)std::max(pl.nsplit, 1) * 2 * 64 * 64);
   pl.d_pcnt = cv.take<unsigned>(std::max(pl.nsplit, 1));
@@ -422,6 +441,7 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
   if (!pl.thin.empty() && (rc = h2d(pl.d_thin, pl.thin.data(), pl.thin.size() * sizeof(ThinUnit), s))) return rc;
+  if (!pl.small.empty() && (rc = h2d(pl.d_small, pl.small.data(), pl.small.size() * sizeof(int), s))) return rc;
   return check_hip("upload");
 }
 
@@ -654,6 +674,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
     if (ngroups && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
   }
+  const bool fuse_small = g_small_fused && qscheme == kMse && !exhaustive && merged && !pl.small.empty() &&
+                          pl.small_groups > 0 && num_attempts <= 1024;
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
@@ -666,8 +688,11 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
       prof_class(1); prof_mark(s);
       // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
-        launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.d_rank0, pl.d_groups,
-                         ngroups, pl.hist_nv, s);
+        launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, fuse_small ? pl.nhist_big : nhist, num_attempts, bits, slot,
+                         pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, s);
+        if (fuse_small)   // the small jobs' search and finalize in one block each
+          launch_mse_small_admm(pl.d_desc, pl.d_small, (int)pl.small.size(), pl.small_groups, num_attempts, bits,
+                                slot, it, pl.d_rank0, pl.d_groups, ngroups, s);
       } else if (!exhaustive) {
         launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.hist_nv, s);
       } else {
@@ -677,7 +702,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
       prof_mark(s);
     }
     prof_class(2); prof_mark(s);
-    launch_finalize_admm(pl.d_desc, pl.d_fin, nfin, pl.fin_elems, num_attempts, bits, qscheme, slot, it, s);
+    launch_finalize_admm(pl.d_desc, pl.d_fin, fuse_small ? pl.nfin_big : nfin, pl.fin_elems, num_attempts, bits,
+                         qscheme, slot, it, s);
     prof_mark(s);
   }
   g_prof.sampled = true;

@@ -96,7 +96,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
 // chain over its 1/KS slice of the k range of every K-step; the partials are summed in
 // fixed order at the end.
-template <int WM, int KS, int NS>
+template <int WM, int KS, int NS, int NA = 1>   // NA: independent accumulator chains per wave (1 or 2)
 __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
                                                         int ntiles, unsigned* __restrict__ queue,
                                                         float* __restrict__ kpart, unsigned* __restrict__ pcnt, int slot,
@@ -182,9 +182,9 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
         if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
       }
 
-      f32x16 acc;
+      f32x16 acc, acc2;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) { acc[r] = 0.f; acc2[r] = 0.f; }
 
       // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
       // stages stay in flight), publish it (barrier), refill the stage consumed one step
@@ -204,10 +204,11 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
       const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                              \
       const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);              \
       const float4 b = *reinterpret_cast<const float4*>(st + boff + cpos);              \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);               \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);               \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);               \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);               \
+      f32x16& ac = (NA == 2 && (qq & 1)) ? acc2 : acc;                                  \
+      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, ac, 0, 0, 0);                 \
+      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, ac, 0, 0, 0);                 \
+      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, ac, 0, 0, 0);                 \
+      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, ac, 0, 0, 0);                 \
     }                                                                                   \
   } while (0)
       const int nfull = nk / NS * NS;
@@ -224,6 +225,10 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
       // the epilogue; drawing earlier would hand tiles out before workers are free)
       if (tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
       __syncthreads();   // nothing in flight any more; the stages may be reused
+      if (NA == 2) {     // the two chains (even / odd fragment groups), summed once
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
+      }
       if (KS > 1) {      // fixed-order reduction of the KS partial accumulators (deterministic)
         if (ks > 0) {
           float* dst = st0 + ((ks - 1) * NSUB + sub) * 1024;
@@ -597,12 +602,17 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
 #define ADMMQ_GEMM(WM, KS, NS, n, t, q)                                                                      \
   hipLaunchKernelGGL((k_gemm<WM, KS, NS>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, d, \
                      t, n, q, kpart, pcnt, slot, iter, eps, ncand)
+#define ADMMQ_GEMM2(WM, KS, NS, n, t, q)                                                                     \
+  hipLaunchKernelGGL((k_gemm<WM, KS, NS, 2>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, \
+                     d, t, n, q, kpart, pcnt, slot, iter, eps, ncand)
   if (ntiles_big > 0) {
     if (gemm_big_wm() == 4) {
       ADMMQ_GEMM(4, 1, 3, ntiles_big, tiles, queue);
     } else {
       switch (cfg_big) {
         case 14: ADMMQ_GEMM(2, 1, 4, ntiles_big, tiles, queue); break;
+        case 113: ADMMQ_GEMM2(2, 1, 3, ntiles_big, tiles, queue); break;
+        case 114: ADMMQ_GEMM2(2, 1, 4, ntiles_big, tiles, queue); break;
         case 15: ADMMQ_GEMM(2, 1, 5, ntiles_big, tiles, queue); break;
         case 16: ADMMQ_GEMM(2, 1, 6, ntiles_big, tiles, queue); break;
         case 24: ADMMQ_GEMM(2, 2, 4, ntiles_big, tiles, queue); break;
@@ -620,6 +630,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int
     }
   }
 #undef ADMMQ_GEMM
+#undef ADMMQ_GEMM2
 }
 
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,

@@ -551,48 +551,17 @@ __device__ void rank_by_counting(const float* thr, float* tsort, unsigned short*
   }
 }
 
-template <int QMAX, int NV>
-__global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                      const Chunk* __restrict__ chunks, int ncand, int slot,
-                                                      const unsigned short* __restrict__ rank0,
-                                                      const unsigned short* __restrict__ groups, int ngroups) {
-  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
-  const Chunk ck = chunks[blockIdx.x];
-  // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
-  // this thread's elements; the descriptor fields are read alongside
-  const int stopped = ck.done ? *ck.done : 0;
-  const float mx = __uint_as_float(ck.stat[4 * slot]);
-  const long long total = ck.total;
-  float4 x4[2 * NV];
-#pragma unroll
-  for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
-    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4[hh] = load_x4(ck.X, ck.U, e);
-  }
-  const MseView& v = mview(d, qj, ck.job);
-  if (stopped) return;
-  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-  if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
-    if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
-    return;
-  }
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int n = ncand;
+// Stage-1 table of one job in LDS (the setup of k_mse_hist3 and k_mse_small_admm): the
+// thresholds in the host's merged order with the tie groups ordered by value, L per
+// (level, candidate), the coarse cell index; the buckets zeroed. Returns the cell scale.
+template <int QMAX>
+__device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short* __restrict__ rank0,
+                                         const unsigned short* __restrict__ groups, int ngroups,
+                                         unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
+                                         unsigned* cntN, float* thr, float* tsort, unsigned short* rnk,
+                                         unsigned short* cell) {
   const int M = QMAX * n;
-  const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
-  unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
-  unsigned long long* sumN = sumA + nb;
-  unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
-  unsigned* cntN = cntA + nb;
-  float* thr = reinterpret_cast<float*>(cntN + nb);                          // M
-  float* tsort = thr + M;                                                    // M
-  unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
-  unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
-  __shared__ double red[8];
-  __shared__ unsigned long long wtot[8], wtot2[8];
-  __shared__ unsigned wtot32[8], wtot32b[8];
-  __shared__ int last;
+  const int nb = M + 1 + 64;
   fill_thresholds(thr, mx, n, QMAX);
   for (int i = threadIdx.x; i < M; i += blockDim.x) rnk[i] = rank0[i];
   for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
@@ -637,6 +606,127 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
       for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
   }
   __syncthreads();
+  return inv;
+}
+
+// Bucket of one element (B = #{thresholds <= |x|}) and its LDS histogram adds.
+__device__ __forceinline__ void h3_insert(float x, float inv, const float* tsort, const unsigned short* cell, int K1,
+                                          int dummy, unsigned long long* sumA, unsigned long long* sumN,
+                                          unsigned* cntA, unsigned* cntN) {
+  const float a = __builtin_fabsf(x);
+  const int g = min(kCells - 1, (int)(a * inv));
+  int B = cell[g];
+  const int hiB = cell[g + 1];
+  while (B < hiB && tsort[B] <= a) ++B;       // B = #{thresholds <= a}
+  const bool live = B > 0;                    // 0: reaches no level for any candidate
+  const int b = live ? B : dummy;
+  const bool neg = x < 0.f;
+  const unsigned long long af = live ? to_fixed(a, K1) : 0ull;
+  atomicAdd(neg ? &sumN[b] : &sumA[b], af);
+  atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
+}
+
+// all = positives + negatives, then suffix sums S[i] = sum over buckets >= i of the four
+// bucket arrays in one block pass: contiguous per-thread runs, then a scan of the run
+// totals over the block (in thread order). Ends with a block barrier.
+__device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
+                                          unsigned* cntN, unsigned long long* wtot, unsigned long long* wtot2,
+                                          unsigned* wtot32, unsigned* wtot32b) {
+  for (int i = threadIdx.x; i <= M; i += blockDim.x) { sumA[i] += sumN[i]; cntA[i] += cntN[i]; }
+  __syncthreads();
+  const int len = M + 1;
+  const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
+  unsigned long long r1 = 0ull, r2 = 0ull;
+  unsigned r3 = 0u, r4 = 0u;
+  for (int i = b1 - 1; i >= b0; --i) {
+    r1 += sumA[i]; sumA[i] = r1;
+    r2 += sumN[i]; sumN[i] = r2;
+    r3 += cntA[i]; cntA[i] = r3;
+    r4 += cntN[i]; cntN[i] = r4;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long q1 = r1, q2 = r2;
+  unsigned q3 = r3, q4 = r4;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
+    const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
+    if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
+  }
+  if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
+  __syncthreads();
+  unsigned long long a1 = 0ull, a2 = 0ull;
+  unsigned a3 = 0u, a4 = 0u;
+  for (int j = w + 1; j < (int)(blockDim.x >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
+  const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
+  const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
+  if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
+  for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
+  __syncthreads();
+}
+
+// Per-candidate level sums T1(c), T2(c) from the suffix-summed buckets (x > 0 reaches at
+// most qmax - 1 levels, so the top level reads the negatives' buckets only).
+template <int QMAX>
+__device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rnk, const unsigned long long* sumA,
+                                          const unsigned long long* sumN, const unsigned* cntA, const unsigned* cntN,
+                                          unsigned long long& t1, unsigned long long& t2) {
+  t1 = 0ull; t2 = 0ull;
+#pragma unroll
+  for (int k = 1; k < QMAX; ++k) {
+    const int L = rnk[(k - 1) * n + c];
+    t1 += sumA[L];
+    t2 += (unsigned long long)(2 * k - 1) * cntA[L];
+  }
+  const int L = rnk[(QMAX - 1) * n + c];
+  t1 += sumN[L];
+  t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
+}
+
+template <int QMAX, int NV>
+__global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+                                                      const Chunk* __restrict__ chunks, int ncand, int slot,
+                                                      const unsigned short* __restrict__ rank0,
+                                                      const unsigned short* __restrict__ groups, int ngroups) {
+  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
+  const Chunk ck = chunks[blockIdx.x];
+  // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
+  // this thread's elements; the descriptor fields are read alongside
+  const int stopped = ck.done ? *ck.done : 0;
+  const float mx = __uint_as_float(ck.stat[4 * slot]);
+  const long long total = ck.total;
+  float4 x4[2 * NV];
+#pragma unroll
+  for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) x4[hh] = load_x4(ck.X, ck.U, e);
+  }
+  const MseView& v = mview(d, qj, ck.job);
+  if (stopped) return;
+  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
+    if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = ncand;
+  const int M = QMAX * n;
+  const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
+  unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
+  unsigned long long* sumN = sumA + nb;
+  unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
+  unsigned* cntN = cntA + nb;
+  float* thr = reinterpret_cast<float*>(cntN + nb);                          // M
+  float* tsort = thr + M;                                                    // M
+  unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
+  unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
+  __shared__ double red[8];
+  __shared__ unsigned long long wtot[8], wtot2[8];
+  __shared__ unsigned wtot32[8], wtot32b[8];
+  __shared__ int last;
+  const float inv = h3_setup<QMAX>(mx, n, rank0, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell);
   const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
@@ -646,71 +736,18 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
     const float4 q4 = x4[j >> 2];
     const float x = (j & 3) == 0 ? q4.x : ((j & 3) == 1 ? q4.y : ((j & 3) == 2 ? q4.z : q4.w));
     s2 += (double)x * (double)x;
-    const float a = __builtin_fabsf(x);
-    const int g = min(kCells - 1, (int)(a * inv));
-    int B = cell[g];
-    const int hiB = cell[g + 1];
-    while (B < hiB && tsort[B] <= a) ++B;       // B = #{thresholds <= a}
-    const bool live = B > 0;                    // 0: reaches no level for any candidate
-    const int b = live ? B : dummy;
-    const bool neg = x < 0.f;
-    const unsigned long long af = live ? to_fixed(a, K1) : 0ull;
-    atomicAdd(neg ? &sumN[b] : &sumA[b], af);
-    atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
+    h3_insert(x, inv, tsort, cell, K1, dummy, sumA, sumN, cntA, cntN);
   }
   __syncthreads();
   const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
-  // all = positives + negatives; then suffix sums S[i] = sum over buckets >= i
-  for (int i = threadIdx.x; i <= M; i += blockDim.x) { sumA[i] += sumN[i]; cntA[i] += cntN[i]; }
-  __syncthreads();
-  {   // suffix sums of the four bucket arrays in one block pass: contiguous per-thread
-      // runs, then a scan of the run totals over the block (in thread order)
-    const int len = M + 1;
-    const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
-    const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
-    unsigned long long r1 = 0ull, r2 = 0ull;
-    unsigned r3 = 0u, r4 = 0u;
-    for (int i = b1 - 1; i >= b0; --i) {
-      r1 += sumA[i]; sumA[i] = r1;
-      r2 += sumN[i]; sumN[i] = r2;
-      r3 += cntA[i]; cntA[i] = r3;
-      r4 += cntN[i]; cntN[i] = r4;
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned long long q1 = r1, q2 = r2;
-    unsigned q3 = r3, q4 = r4;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
-      const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
-      if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
-    }
-    if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
-    __syncthreads();
-    unsigned long long a1 = 0ull, a2 = 0ull;
-    unsigned a3 = 0u, a4 = 0u;
-    for (int j = w + 1; j < (int)(blockDim.x >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
-    const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
-    const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
-    if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
-    for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
-    __syncthreads();
-  }
+  h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
   // per-candidate totals of this block into one of kHistRep replicas
   const int rep = blockIdx.x & (kHistRep - 1);
   unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
   unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
   for (int c = threadIdx.x; c < n; c += blockDim.x) {
-    unsigned long long t1 = 0ull, t2 = 0ull;
-#pragma unroll
-    for (int k = 1; k < QMAX; ++k) {
-      const int L = rnk[(k - 1) * n + c];
-      t1 += sumA[L];
-      t2 += (unsigned long long)(2 * k - 1) * cntA[L];
-    }
-    const int L = rnk[(QMAX - 1) * n + c];
-    t1 += sumN[L];
-    t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
+    unsigned long long t1, t2;
+    h3_totals<QMAX>(c, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
     if (t1) atomicAdd(&g1[c], t1);
     if (t2) atomicAdd(&g2[c], t2);
   }
@@ -763,6 +800,178 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
   __syncthreads();
   sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
   trace(__builtin_amdgcn_s_memrealtime());
+}
+
+// Small ADMM jobs (thin factors, I <= kThinRows: the 9-row spatial mode of a 3x3 conv,
+// at most 24 k elements): one 1024-thread block per job runs stage 1 over all of the job's
+// elements with the histograms kept in LDS, the candidate selection, stage 2 when
+// |S| > 1, and then k_finalize_admm's step for the same elements - no cross-block
+// flush, ticket, or separate finalize launch (the three were ~30 us of latency per
+// iteration for ~10 k elements). Same integers and the same float32 operations as the
+// multi-block path (the histograms are exact sums; S2 only sets the rigorous bounds).
+template <int QMAX, int G>   // G: float4 groups per thread (1024 threads x 4 G elements cover the job)
+__global__ __launch_bounds__(1024) void k_mse_small_admm(const ProbDesc* __restrict__ d, const int* __restrict__ jobs,
+                                                         int ncand, int bits, int slot, int iter,
+                                                         const unsigned short* __restrict__ rank0,
+                                                         const unsigned short* __restrict__ groups, int ngroups) {
+  const ProbDesc& p = d[jobs[blockIdx.x]];
+  const long long total = (long long)p.I * p.ld;
+  // every element of the job is loaded up front (H_T, U for the search; H, F too for the
+  // finalize step): their latency overlaps the threshold-table setup
+  float4 t4[G], u4[G], h4[G], f4[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const long long e = 4LL * threadIdx.x + 4096LL * g;
+    t4[g] = make_float4(0.f, 0.f, 0.f, 0.f); u4[g] = t4[g]; h4[g] = t4[g]; f4[g] = t4[g];
+    if (e < total) {
+      t4[g] = *reinterpret_cast<const float4*>(p.HT + e);
+      u4[g] = *reinterpret_cast<const float4*>(p.U + e);
+      h4[g] = *reinterpret_cast<const float4*>(p.H + e);
+      f4[g] = *reinterpret_cast<const float4*>(p.Fp + e);
+    }
+  }
+  if (p.flags[0]) return;   // converged earlier (sticky break)
+  const MseView& v = p.mv;
+  const float mx = __uint_as_float(v.stat[4 * slot]);
+  int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ unsigned long long wtot[16], wtot2[16];
+  __shared__ unsigned wtot32[16], wtot32b[16];
+  __shared__ double red[16];
+  __shared__ int lsel[2 + kMaxSel];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+  if (!mse_degenerate(mx)) {
+    const int n = ncand;
+    const int M = QMAX * n;
+    const int nb = M + 1 + 64;
+    unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);
+    unsigned long long* sumN = sumA + nb;
+    unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
+    unsigned* cntN = cntA + nb;
+    float* thr = reinterpret_cast<float*>(cntN + nb);
+    float* tsort = thr + M;
+    unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);
+    unsigned short* cell = rnk + ((M + 1) & ~1);
+    const float inv = h3_setup<QMAX>(mx, n, rank0, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell);
+    const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
+    const int dummy = M + 1 + lane;
+    double s2 = 0.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float xs[4] = {t4[g].x - u4[g].x, t4[g].y - u4[g].y, t4[g].z - u4[g].z, t4[g].w - u4[g].w};   // H_T - U
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s2 += (double)xs[k] * (double)xs[k];
+        h3_insert(xs[k], inv, tsort, cell, K1, dummy, sumA, sumN, cntA, cntN);
+      }
+    }
+    __syncthreads();
+    h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
+    unsigned long long t1 = 0ull, t2 = 0ull;   // candidate tid (n <= 1024)
+    if ((int)threadIdx.x < n) h3_totals<QMAX>(threadIdx.x, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+    if (lane == 0) red[w] = s2;
+    __syncthreads();   // every thread is done with the buckets: T1/T2 go where they were
+    unsigned long long* T1v = sumA;
+    unsigned long long* T2v = sumN;
+    if ((int)threadIdx.x < n) { T1v[threadIdx.x] = t1; T2v[threadIdx.x] = t2; }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      double S2 = 0.0;
+      for (int k = 0; k < nw; ++k) S2 += red[k];
+      select_wave2(v, sel, lsel, T1v, T2v, S2, mx, n, QMAX);
+    }
+    __syncthreads();
+    sse_in_block(v, lsel, n, bits, slot, mx, reinterpret_cast<float4*>(smem));
+    __syncthreads();
+  }
+  // k_finalize_admm's step (source/admm.py:59-65) with the chosen scale
+  const QParams qp = block_qparams(kMse, bits, v, slot, ncand, 0, 0.f, 0.f);
+  const float rho = p.rho[0];
+  double s1 = 0.0, s2r = 0.0, s3 = 0.0, s4 = 0.0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const long long e = 4LL * threadIdx.x + 4096LL * g;
+    if (e >= total) continue;
+    const int row = (int)(e / p.ld);
+    const int c0 = (int)(e - (long long)row * p.ld);
+    const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w}, hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w};
+    const float us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w}, fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
+    float ho[4], uo[4], po[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (c0 + k < p.R) {
+        const float xk = ts[k] - us[k];                   // H_T - U
+        const float hn = apply_quant(xk, qp);             // H = quantize(H_T - U)
+        const float dh = hn - ts[k];
+        const float un = us[k] + dh;                      // U += H - H_T
+        ho[k] = hn; uo[k] = un;
+        po[k] = fs[k] + rho * (hn + un);                  // next rhs F + rho(H+U)
+        const float dp = hn - hs[k];
+        s1 += (double)(dh * dh); s2r += (double)(hn * hn);
+        s3 += (double)(dp * dp); s4 += (double)(un * un);
+      } else {
+        ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
+      }
+    }
+    *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
+    *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
+    *reinterpret_cast<float4*>(p.P + e) = make_float4(po[0], po[1], po[2], po[3]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off); s2r += __shfl_xor(s2r, off);
+    s3 += __shfl_xor(s3, off); s4 += __shfl_xor(s4, off);
+  }
+  __shared__ double fred[16][4];
+  if (lane == 0) { fred[w][0] = s1; fred[w][1] = s2r; fred[w][2] = s3; fred[w][3] = s4; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double t = 0.0;
+    for (int k = 0; k < nw; ++k) t += fred[k][threadIdx.x];
+    atomicAdd(&p.res[4 * (kResRep * slot) + threadIdx.x], t);
+  }
+  if (threadIdx.x == 0) {
+    p.flags[1] = iter + 1;
+    unsigned* st = p.mv.stat + 4 * (slot ^ 1);
+    st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
+    double* rs = p.res + 4 * kResRep * (slot ^ 1);
+    for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
+  }
+}
+
+// maxtotal: the largest I * ld among the jobs (picks G); 0 when the path cannot run
+int small_admm_groups(long long maxtotal) {
+  const long long g = (maxtotal + 4095) / 4096;
+  return g <= 1 ? 1 : (g <= 2 ? 2 : (g <= 3 ? 3 : (g <= 4 ? 4 : (g <= 6 ? 6 : 0))));
+}
+
+void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ngr, int ncand, int bits, int slot,
+                           int iter, const unsigned short* rank0, const unsigned short* groups, int ngroups,
+                           hipStream_t s) {
+  if (njobs <= 0) return;
+  const size_t lds = hist3_lds_bytes(ncand, bits);
+#define ADMMQ_SMG(Q, GG) \
+  hipLaunchKernelGGL((k_mse_small_admm<Q, GG>), dim3(njobs), dim3(1024), lds, s, d, jobs, ncand, bits, slot, iter, \
+                     rank0, groups, ngroups)
+#define ADMMQ_SM(Q)                        \
+  switch (ngr) {                           \
+    case 1: ADMMQ_SMG(Q, 1); break;        \
+    case 2: ADMMQ_SMG(Q, 2); break;        \
+    case 3: ADMMQ_SMG(Q, 3); break;        \
+    case 4: ADMMQ_SMG(Q, 4); break;        \
+    default: ADMMQ_SMG(Q, 6); break;       \
+  }
+  switch (bits) {
+    case 1: ADMMQ_SM(1); break;
+    case 2: ADMMQ_SM(2); break;
+    case 3: ADMMQ_SM(4); break;
+    case 4: ADMMQ_SM(8); break;
+    default: ADMMQ_SM(16); break;
+  }
+#undef ADMMQ_SM
+#undef ADMMQ_SMG
 }
 
 size_t hist3_lds_bytes(int ncand, int bits) {

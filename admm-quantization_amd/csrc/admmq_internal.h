@@ -148,6 +148,7 @@ int copy_thin_trace(unsigned long long* host, int n);
 int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
+int copy_setup_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
 int check_thresholds(unsigned seed, int nsamp);
 bool merged_ok(int ncand, int bits);

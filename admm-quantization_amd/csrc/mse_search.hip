@@ -551,6 +551,18 @@ __device__ void rank_by_counting(const float* thr, float* tsort, unsigned short*
   }
 }
 
+// Diagnostics: s_memrealtime stamps inside the stage-1 table setup of the last launch, per
+// block {start, thresholds + host order in LDS, ties ordered, L, cells} (admmq_debug_setup_trace).
+constexpr int kSetupTraceMax = 4096;
+__device__ unsigned long long g_setup_trace[kSetupTraceMax][5];
+int copy_setup_trace(unsigned long long* host, int n) {
+  n = n < kSetupTraceMax ? n : kSetupTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
+#define ADMMQ_SETUP_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < kSetupTraceMax) g_setup_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+
 // Stage-1 table of one job in LDS (the setup of k_mse_hist3 and k_mse_small_admm): the
 // thresholds in the host's merged order with the tie groups ordered by value, L per
 // (level, candidate), the coarse cell index; the buckets zeroed. Returns the cell scale.
@@ -562,10 +574,24 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
                                          unsigned short* cell) {
   const int M = QMAX * n;
   const int nb = M + 1 + 64;
+  ADMMQ_SETUP_STAMP(0);
+  // the host order is loaded before the thresholds are computed, so its latency overlaps them
+  constexpr int kR0 = (kMaxMerged + 511) / 512;   // per thread, for blocks of >= 512 threads
+  unsigned short r0v[kR0];
+#pragma unroll
+  for (int j = 0; j < kR0; ++j) {
+    const int i = threadIdx.x + j * (int)blockDim.x;
+    r0v[j] = i < M ? rank0[i] : (unsigned short)0;
+  }
   fill_thresholds(thr, mx, n, QMAX);
-  for (int i = threadIdx.x; i < M; i += blockDim.x) rnk[i] = rank0[i];
+#pragma unroll
+  for (int j = 0; j < kR0; ++j) {
+    const int i = threadIdx.x + j * (int)blockDim.x;
+    if (i < M) rnk[i] = r0v[j];
+  }
   for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
   __syncthreads();
+  ADMMQ_SETUP_STAMP(1);
   for (int e = threadIdx.x; e < M; e += blockDim.x) tsort[rnk[e]] = thr[e];
   __syncthreads();
   for (int g = threadIdx.x; g < ngroups; g += blockDim.x) {   // exact-key ties: order by actual value
@@ -582,6 +608,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
     for (int j = 0; j < m; ++j) { tsort[r0 + j] = vs[j]; rnk[es[j]] = (unsigned short)(r0 + j); }
   }
   __syncthreads();
+  ADMMQ_SETUP_STAMP(2);
   int bad = 0;
   for (int r = threadIdx.x; r + 1 < M; r += blockDim.x) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
   if (__syncthreads_or(bad)) {
@@ -595,6 +622,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
     }
   }
   __syncthreads();
+  ADMMQ_SETUP_STAMP(3);
   // coarse index: cell(v) = min(kCells-1, (int)(v * inv)) is non-decreasing in v, so
   // thresholds in cells below cell(a) are < a and those above are > a
   const float inv = (float)kCells / tsort[M - 1];
@@ -606,6 +634,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
       for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
   }
   __syncthreads();
+  ADMMQ_SETUP_STAMP(4);
   return inv;
 }
 

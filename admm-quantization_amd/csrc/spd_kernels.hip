@@ -29,6 +29,23 @@ __device__ __forceinline__ void store_block(double* A, int ldm, int bi, int bj, 
   }
 }
 
+// A 32x32 block through registers (blocks of 256 threads: 4 doubles each), so the next
+// block's loads can be in flight while the current one is multiplied.
+__device__ __forceinline__ void load_regs(double r[4], const double* A, int ldm, int bi, int bj) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = threadIdx.x + 256 * q;
+    r[q] = A[(size_t)(bi * NB + (t >> 5)) * ldm + bj * NB + (t & 31)];
+  }
+}
+__device__ __forceinline__ void store_regs(double* dst, const double r[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = threadIdx.x + 256 * q;
+    dst[(t >> 5) * LS + (t & 31)] = r[q];
+  }
+}
+
 // In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed.
 __device__ void chol32(double* a, int* err) {
   for (int c = 0; c < NB; ++c) {
@@ -162,10 +179,14 @@ __global__ __launch_bounds__(256) void k_linv_row(const ProbDesc* __restrict__ p
     return;
   }
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  // the blocks of step t + 1 are loaded into registers while step t multiplies
+  double ra[4], rb[4];
+  if (j < i) { load_regs(ra, p.A64, p.ldm, i, j); load_regs(rb, p.L64, p.ldm, j, j); }
   for (int t = j; t < i; ++t) {
-    load_block(ta, p.A64, p.ldm, i, t);   // L_it
-    load_block(tb, p.L64, p.ldm, t, j);   // Linv_tj
+    store_regs(ta, ra);   // L_it
+    store_regs(tb, rb);   // Linv_tj
     __syncthreads();
+    if (t + 1 < i) { load_regs(ra, p.A64, p.ldm, i, t + 1); load_regs(rb, p.L64, p.ldm, t + 1, j); }
     mm_nn(ta, tb, acc);
     __syncthreads();
   }
@@ -193,10 +214,14 @@ __global__ __launch_bounds__(256) void k_minv(const ProbDesc* __restrict__ probs
   const int j = q - i * (i + 1) / 2;      // j <= i
   __shared__ double ta[NB * LS], tb[NB * LS];
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double ra[4], rb[4];
+  load_regs(ra, p.L64, p.ldm, i, i);
+  load_regs(rb, p.L64, p.ldm, i, j);
   for (int t = i; t < n; ++t) {
-    load_block(ta, p.L64, p.ldm, t, i);   // Linv_ti
-    load_block(tb, p.L64, p.ldm, t, j);   // Linv_tj
+    store_regs(ta, ra);   // Linv_ti
+    store_regs(tb, rb);   // Linv_tj
     __syncthreads();
+    if (t + 1 < n) { load_regs(ra, p.L64, p.ldm, t + 1, i); load_regs(rb, p.L64, p.ldm, t + 1, j); }
     mm_tn(ta, tb, acc);
     __syncthreads();
   }

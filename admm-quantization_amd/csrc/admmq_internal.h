@@ -105,6 +105,23 @@ struct Chunk {
   long long total;
 };
 
+// Loads through global (not flat) pointers: flat loads also count in lgkmcnt, and a
+// kernel prologue that issues all its loads before using any needs plain vmcnt order.
+typedef __attribute__((address_space(1))) const float gcf32;
+typedef __attribute__((address_space(1))) const int gci32;
+typedef float gf32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float* q) {
+  const gf32x4 v = *(__attribute__((address_space(1))) const gf32x4*)q;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int gld_i32(const int* q) { return *(gci32*)q; }
+__device__ __forceinline__ unsigned gld_u32(const unsigned* q) {
+  return *(__attribute__((address_space(1))) const unsigned*)q;
+}
+__device__ __forceinline__ float4 sub4(float4 a, float4 b) {
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+
 // Quantizer input elements at off..off+3: X, or H_T - U for an ADMM view (the GEMM
 // does not store X = H_T - U; every reader forms it with the same float32 subtraction).
 __device__ __forceinline__ float4 load_x4(const float* X, const float* U, long long off) {
@@ -149,6 +166,7 @@ int copy_gemm_trace(unsigned long long* host, int n);
 int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
+int copy_small_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
 int check_thresholds(unsigned seed, int nsamp);
 bool merged_ok(int ncand, int bits);

@@ -717,6 +717,7 @@ int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return cop
 int32_t admmq_debug_thin_trace(unsigned long long* host, int32_t n) { return copy_thin_trace(host, n); }
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
+int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }
 

@@ -71,6 +71,7 @@ int copy_hist_trace(unsigned long long* host, int n) {
 // Diagnostics: how often the selection leaves more than one candidate ({|S| == 1,
 // 2..kMaxSel, exhaustive} counts since the last reset), for admmq_debug_sel_stats.
 __device__ unsigned long long g_sel_stats[3];
+__device__ int g_no_stop = 0;   // stop flag of units without one (standalone quantization)
 int copy_sel_stats(unsigned long long* host, int reset) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sel_stats), sizeof(g_sel_stats)) != hipSuccess) return -1;
   if (reset) {
@@ -105,9 +106,9 @@ __device__ __forceinline__ float level_threshold_fast(float s, int k) {
 
 // Threshold table of one job into LDS: thr[(k-1) n + c] = smallest a with
 // |q_c(a)| >= k, for k = 1..qmax (increasing in c and in k).
-__device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax) {
+__device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax, int nt) {
   const float den = (float)(2 * qmax - 1);
-  for (int e = threadIdx.x; e < qmax * n; e += blockDim.x) {
+  for (int e = threadIdx.x; e < qmax * n; e += nt) {
     const int k = 1 + e / n, c = e - (k - 1) * n;
     thr[e] = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
   }
@@ -302,8 +303,8 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
     x4v[g] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < total) x4v[g] = load_x4(v.X, v.U, e);
   }
-  fill_thresholds(thr, mx, n, QMAX);
-  if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX); }
+  fill_thresholds(thr, mx, n, QMAX, blockDim.x);
+  if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX, blockDim.x); }
   for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
   __syncthreads();
   const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
@@ -459,7 +460,9 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
 // A coarse index cnt[g] = #{thresholds in cells < g} over kCells equal cells of
 // [0, max threshold] then turns B(a) into two independent LDS reads and a walk of
 // the few thresholds of a's cell.
-constexpr int kCells = 2048;
+constexpr int kCells = 4096;
+constexpr int kH3Threads = 512;       // k_mse_hist3 block (its helpers take the size as a constant:
+constexpr int kSmallThreads = 1024;   // k_mse_small_admm block  reading blockDim is a global load)
 
 // Candidate selection from per-candidate totals T1/T2 (LDS) and S2, by one wave:
 // as select_wave, without the suffix scan.
@@ -512,6 +515,48 @@ __device__ void select_wave2(const MseView& v, int* sel, int* lsel, const unsign
   }
 }
 
+// The same selection by the whole block, one candidate per thread (n <= blockDim.x):
+// thread c holds T1(c), T2(c) in registers; the bounds are computed once per candidate
+// (the one-wave form walks ceil(n/64) candidates per lane twice, a serial fp64 chain of
+// ~4 us); min(A + E) and the ascending list of S come from block reductions. Ends with
+// a block barrier (lsel visible to every thread).
+__device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned long long t1, unsigned long long t2,
+                             double S2, float mx, int n, int qmax) {
+  __shared__ double wmin[16];
+  __shared__ int wcnt[16];
+  const int c = threadIdx.x, lane = c & 63, w = c >> 6, nw = (int)(blockDim.x >> 6);
+  SelCtx cx;
+  cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * qmax - 1);
+  cx.u = 0x1p-24;
+  cx.fixu = ldexp(1.0, -hist_fixed_exp(mx, v.nelem, qmax));
+  cx.Kterm = (double)v.nq * ldexp(1.0, -fixed_exp(mx, v.nq));
+  cx.Nterm = (double)((long long)v.nelem * qmax);
+  cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
+  double lo = 1e300, hi = 1e300;
+  if (c < n) cx.bounds(c, t1, t2, lo, hi);
+  double m = hi;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off));
+  if (lane == 0) wmin[w] = m;
+  __syncthreads();
+  double mn = wmin[0];
+  for (int k = 1; k < nw; ++k) mn = fmin(mn, wmin[k]);
+  const bool keep = c < n && lo <= mn;
+  const unsigned long long bal = __ballot(keep);
+  if (lane == 0) wcnt[w] = __popcll(bal);
+  __syncthreads();
+  int pos = __popcll(bal & ((1ull << lane) - 1ull)), total = 0;
+  for (int k = 0; k < nw; ++k) { pos += k < w ? wcnt[k] : 0; total += wcnt[k]; }
+  if (keep && pos < kMaxSel) { sel[2 + pos] = c; lsel[2 + pos] = c; }
+  if (c == 0) {
+    if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
+    else { sel[0] = total; sel[1] = 0; }
+    lsel[0] = sel[0]; lsel[1] = sel[1];
+    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+  }
+  __syncthreads();
+}
+
 
 // Rank-by-counting of the thresholds (fallback when the host order does not hold):
 // rows thr[j][.] are non-decreasing; with the order (value, level, candidate)
@@ -560,42 +605,72 @@ int copy_setup_trace(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess
              ? n : -1;
 }
+// Phase stamps of k_mse_small_admm's blocks (last launch): {start, loads+flag, setup,
+// insert, suffix, select, stage 2, end} and the selected-list length (admmq_debug_small_trace).
+constexpr int kSmallTraceMax = 64;
+__device__ unsigned long long g_small_trace[kSmallTraceMax][9];
+int copy_small_trace(unsigned long long* host, int n) {
+  n = n < kSmallTraceMax ? n : kSmallTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_small_trace), (size_t)n * 9 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
+#define ADMMQ_SMALL_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
 #define ADMMQ_SETUP_STAMP(k) \
   if (threadIdx.x == 0 && blockIdx.x < kSetupTraceMax) g_setup_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+
+// The global inputs of the stage-1 table setup that do not depend on max|x|: this
+// thread's entries of the host order of the thresholds (blocks of >= 512 threads) and
+// its tie group (packed 6 x u16). The kernels issue these loads before their element
+// loads: vector loads complete in issue order, so issued after the elements any wait for
+// them would wait for all of the elements too.
+constexpr int kR0 = (kMaxMerged + 511) / 512;
+struct H3Pre {
+  unsigned short r0v[kR0];
+  unsigned gw[3];
+};
+__device__ __forceinline__ void h3_load_order(const unsigned short* __restrict__ rank0, int M,
+                                              const unsigned short* __restrict__ groups, int ngroups, H3Pre& pre, int nt) {
+  // unconditional loads (clamped index; entries past M / ngroups are ignored), so the
+  // compiler's wait counts stay exact: rank0 holds kMaxMerged entries and groups
+  // kMaxMerged / 2 groups of 12 B (4-byte aligned), whatever M and ngroups are
+#pragma unroll
+  for (int j = 0; j < kR0; ++j) {
+    const int i = threadIdx.x + j * nt;
+    pre.r0v[j] = rank0[min(i, M - 1)];
+  }
+  const unsigned* g32 = reinterpret_cast<const unsigned*>(groups + 6 * min((int)threadIdx.x, kMaxMerged / 2 - 1));
+  pre.gw[0] = g32[0]; pre.gw[1] = g32[1]; pre.gw[2] = g32[2];
+  (void)ngroups;
+}
 
 // Stage-1 table of one job in LDS (the setup of k_mse_hist3 and k_mse_small_admm): the
 // thresholds in the host's merged order with the tie groups ordered by value, L per
 // (level, candidate), the coarse cell index; the buckets zeroed. Returns the cell scale.
 template <int QMAX>
-__device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short* __restrict__ rank0,
+__device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
                                          const unsigned short* __restrict__ groups, int ngroups,
                                          unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
                                          unsigned* cntN, float* thr, float* tsort, unsigned short* rnk,
-                                         unsigned short* cell) {
+                                         unsigned short* cell, int nt) {
   const int M = QMAX * n;
   const int nb = M + 1 + 64;
   ADMMQ_SETUP_STAMP(0);
-  // the host order is loaded before the thresholds are computed, so its latency overlaps them
-  constexpr int kR0 = (kMaxMerged + 511) / 512;   // per thread, for blocks of >= 512 threads
-  unsigned short r0v[kR0];
+  fill_thresholds(thr, mx, n, QMAX, nt);   // overlaps the latency of the order (and element) loads
 #pragma unroll
   for (int j = 0; j < kR0; ++j) {
-    const int i = threadIdx.x + j * (int)blockDim.x;
-    r0v[j] = i < M ? rank0[i] : (unsigned short)0;
+    const int i = threadIdx.x + j * nt;
+    if (i < M) rnk[i] = pre.r0v[j];
   }
-  fill_thresholds(thr, mx, n, QMAX);
-#pragma unroll
-  for (int j = 0; j < kR0; ++j) {
-    const int i = threadIdx.x + j * (int)blockDim.x;
-    if (i < M) rnk[i] = r0v[j];
-  }
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
+  for (int i = threadIdx.x; i < nb; i += nt) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
   __syncthreads();
   ADMMQ_SETUP_STAMP(1);
-  for (int e = threadIdx.x; e < M; e += blockDim.x) tsort[rnk[e]] = thr[e];
+  for (int e = threadIdx.x; e < M; e += nt) tsort[rnk[e]] = thr[e];
   __syncthreads();
-  for (int g = threadIdx.x; g < ngroups; g += blockDim.x) {   // exact-key ties: order by actual value
-    const unsigned short* gr = groups + 6 * g;
+  // exact-key ties: order by actual value (the thread's first group was prefetched; a
+  // load in the same loop would, after the join, make the compiler wait for every
+  // outstanding load, the elements included)
+  auto tie_group = [&](const unsigned short* gr) {
     const int r0 = gr[0], m = gr[1];
     int es[4];
     float vs[4];
@@ -606,15 +681,23 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
         const int te = es[j]; es[j] = es[j - 1]; es[j - 1] = te;
       }
     for (int j = 0; j < m; ++j) { tsort[r0 + j] = vs[j]; rnk[es[j]] = (unsigned short)(r0 + j); }
+  };
+  if ((int)threadIdx.x < ngroups) {
+    const unsigned short gr[6] = {(unsigned short)(pre.gw[0] & 0xFFFFu), (unsigned short)(pre.gw[0] >> 16),
+                                  (unsigned short)(pre.gw[1] & 0xFFFFu), (unsigned short)(pre.gw[1] >> 16),
+                                  (unsigned short)(pre.gw[2] & 0xFFFFu), (unsigned short)(pre.gw[2] >> 16)};
+    tie_group(gr);
   }
+  if (ngroups > nt)
+    for (int g = threadIdx.x + nt; g < ngroups; g += nt) tie_group(groups + 6 * g);
   __syncthreads();
   ADMMQ_SETUP_STAMP(2);
   int bad = 0;
-  for (int r = threadIdx.x; r + 1 < M; r += blockDim.x) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
+  for (int r = threadIdx.x; r + 1 < M; r += nt) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
   if (__syncthreads_or(bad)) {
     rank_by_counting(thr, tsort, rnk, mx, n, QMAX);   // never expected; exact either way
   } else {
-    for (int e = threadIdx.x; e < M; e += blockDim.x) {   // L = 1 + index of the last equal value
+    for (int e = threadIdx.x; e < M; e += nt) {   // L = 1 + index of the last equal value
       const int r = rnk[e];
       int l = r + 1;
       while (l < M && tsort[l] == tsort[r]) ++l;
@@ -626,7 +709,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
   // coarse index: cell(v) = min(kCells-1, (int)(v * inv)) is non-decreasing in v, so
   // thresholds in cells below cell(a) are < a and those above are > a
   const float inv = (float)kCells / tsort[M - 1];
-  for (int r = threadIdx.x; r < M; r += blockDim.x) {
+  for (int r = threadIdx.x; r < M; r += nt) {
     const int cr = min(kCells - 1, (int)(tsort[r] * inv));
     const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * inv));
     for (int g = cp + 1; g <= cr; ++g) cell[g] = (unsigned short)r;
@@ -638,21 +721,46 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const unsigned short*
   return inv;
 }
 
-// Bucket of one element (B = #{thresholds <= |x|}) and its LDS histogram adds.
-__device__ __forceinline__ void h3_insert(float x, float inv, const float* tsort, const unsigned short* cell, int K1,
-                                          int dummy, unsigned long long* sumA, unsigned long long* sumN,
-                                          unsigned* cntA, unsigned* cntN) {
-  const float a = __builtin_fabsf(x);
-  const int g = min(kCells - 1, (int)(a * inv));
-  int B = cell[g];
-  const int hiB = cell[g + 1];
-  while (B < hiB && tsort[B] <= a) ++B;       // B = #{thresholds <= a}
-  const bool live = B > 0;                    // 0: reaches no level for any candidate
-  const int b = live ? B : dummy;
-  const bool neg = x < 0.f;
-  const unsigned long long af = live ? to_fixed(a, K1) : 0ull;
-  atomicAdd(neg ? &sumN[b] : &sumA[b], af);
-  atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
+// Buckets B = #{thresholds <= |x|} of N elements and their LDS histogram adds, in phases whose LDS reads are independent across the
+// elements (so their latencies overlap instead of chaining element after element): the
+// two cell bounds, then three threshold probes, then the walk for an element whose cell
+// still holds more thresholds <= |x| (rare), then the histogram adds.
+template <int N>
+__device__ __forceinline__ void h3_insert_n(const float* xs, float inv, const float* tsort, const unsigned short* cell,
+                                            int M, int K1, int dummy, unsigned long long* sumA,
+                                            unsigned long long* sumN, unsigned* cntA, unsigned* cntN) {
+  float a[N];
+  int B[N], hi[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    a[j] = __builtin_fabsf(xs[j]);
+    const int g = min(kCells - 1, (int)(a[j] * inv));
+    B[j] = cell[g];
+    hi[j] = cell[g + 1];
+  }
+  bool more[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int b0 = B[j];
+    const float p0 = tsort[min(b0, M - 1)], p1 = tsort[min(b0 + 1, M - 1)], p2 = tsort[min(b0 + 2, M - 1)];
+    const int cnt = (b0 < hi[j] && p0 <= a[j] ? 1 : 0) + (b0 + 1 < hi[j] && p1 <= a[j] ? 1 : 0) +
+                    (b0 + 2 < hi[j] && p2 <= a[j] ? 1 : 0);   // sorted: the prefix of <= a
+    B[j] = b0 + cnt;
+    more[j] = cnt == 3;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (more[j])
+      while (B[j] < hi[j] && tsort[B[j]] <= a[j]) ++B[j];   // B = #{thresholds <= a}
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const bool live = B[j] > 0;
+    const int b = live ? B[j] : dummy;
+    const bool neg = xs[j] < 0.f;
+    const unsigned long long af = live ? to_fixed(a[j], K1) : 0ull;
+    atomicAdd(neg ? &sumN[b] : &sumA[b], af);
+    atomicAdd(neg ? &cntN[b] : &cntA[b], live ? 1u : 0u);
+  }
 }
 
 // all = positives + negatives, then suffix sums S[i] = sum over buckets >= i of the four
@@ -660,19 +768,19 @@ __device__ __forceinline__ void h3_insert(float x, float inv, const float* tsort
 // totals over the block (in thread order). Ends with a block barrier.
 __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
                                           unsigned* cntN, unsigned long long* wtot, unsigned long long* wtot2,
-                                          unsigned* wtot32, unsigned* wtot32b) {
-  for (int i = threadIdx.x; i <= M; i += blockDim.x) { sumA[i] += sumN[i]; cntA[i] += cntN[i]; }
-  __syncthreads();
+                                          unsigned* wtot32, unsigned* wtot32b, int nt) {
   const int len = M + 1;
-  const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int per = (len + nt - 1) / nt;
   const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
   unsigned long long r1 = 0ull, r2 = 0ull;
   unsigned r3 = 0u, r4 = 0u;
-  for (int i = b1 - 1; i >= b0; --i) {
-    r1 += sumA[i]; sumA[i] = r1;
-    r2 += sumN[i]; sumN[i] = r2;
-    r3 += cntA[i]; cntA[i] = r3;
-    r4 += cntN[i]; cntN[i] = r4;
+  for (int i = b1 - 1; i >= b0; --i) {   // the thread's own run: all = positives + negatives here
+    const unsigned long long sn = sumN[i];
+    const unsigned cn = cntN[i];
+    r1 += sumA[i] + sn; sumA[i] = r1;
+    r2 += sn; sumN[i] = r2;
+    r3 += cntA[i] + cn; cntA[i] = r3;
+    r4 += cn; cntN[i] = r4;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long q1 = r1, q2 = r2;
@@ -687,7 +795,7 @@ __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsig
   __syncthreads();
   unsigned long long a1 = 0ull, a2 = 0ull;
   unsigned a3 = 0u, a4 = 0u;
-  for (int j = w + 1; j < (int)(blockDim.x >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
+  for (int j = w + 1; j < (nt >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
   const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
   const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
   if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
@@ -714,23 +822,33 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
 }
 
 template <int QMAX, int NV>
-__global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
+__global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
                                                       const Chunk* __restrict__ chunks, int ncand, int slot,
                                                       const unsigned short* __restrict__ rank0,
                                                       const unsigned short* __restrict__ groups, int ngroups) {
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   const Chunk ck = chunks[blockIdx.x];
   // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
-  // this thread's elements; the descriptor fields are read alongside
-  const int stopped = ck.done ? *ck.done : 0;
-  const float mx = __uint_as_float(ck.stat[4 * slot]);
+  // the threshold order, this thread's elements - all issued before any is used
+  // (straight-line global loads; past the end a clamped address, zeroed below)
+  const int stopped = gld_i32(ck.done ? ck.done : &g_no_stop);
+  const float mx = __uint_as_float(gld_u32(ck.stat + 4 * slot));
   const long long total = ck.total;
-  float4 x4[2 * NV];
+  H3Pre pre;
+  h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kH3Threads);
+  asm volatile("" ::: "memory");   // issue order: the loads above before the element loads
+  float4 x4[2 * NV], u4[2 * NV];
 #pragma unroll
   for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
-    x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) x4[hh] = load_x4(ck.X, ck.U, e);
+    x4[hh] = gld4(ck.X + (e < total ? e : 0));
+  }
+  if (ck.U) {
+#pragma unroll
+    for (int hh = 0; hh < 2 * NV; ++hh) {
+      const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+      u4[hh] = gld4(ck.U + (e < total ? e : 0));
+    }
   }
   const MseView& v = mview(d, qj, ck.job);
   if (stopped) return;
@@ -755,21 +873,27 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
   __shared__ unsigned long long wtot[8], wtot2[8];
   __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
-  const float inv = h3_setup<QMAX>(mx, n, rank0, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell);
+  const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell, kH3Threads);
   const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
+#pragma unroll
+  for (int hh = 0; hh < 2 * NV; ++hh) {   // X - U (ADMM: H_T - U); zero past the end
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+    if (ck.U) x4[hh] = sub4(x4[hh], u4[hh]);
+    if (e >= total) x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   double s2 = 0.0;
 #pragma unroll
-  for (int j = 0; j < 8 * NV; ++j) {
-    const float4 q4 = x4[j >> 2];
-    const float x = (j & 3) == 0 ? q4.x : ((j & 3) == 1 ? q4.y : ((j & 3) == 2 ? q4.z : q4.w));
-    s2 += (double)x * (double)x;
-    h3_insert(x, inv, tsort, cell, K1, dummy, sumA, sumN, cntA, cntN);
+  for (int hb = 0; hb < 2 * NV; hb += 2) {
+    const float xs[8] = {x4[hb].x, x4[hb].y, x4[hb].z, x4[hb].w, x4[hb + 1].x, x4[hb + 1].y, x4[hb + 1].z, x4[hb + 1].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
+    h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
   }
   __syncthreads();
   const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
-  h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
+  h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b, kH3Threads);
   // per-candidate totals of this block into one of kHistRep replicas
   const int rep = blockIdx.x & (kHistRep - 1);
   unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
@@ -806,10 +930,28 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
   };
   if (!last) { trace(T3); return; }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  unsigned long long* T1v = sumA;                 // reuse LDS: n each
-  unsigned long long* T2v = sumN;
   const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
   const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
+  __shared__ int lsel[2 + kMaxSel];
+  if (n <= (int)blockDim.x) {
+    const int c = threadIdx.x;
+    unsigned long long t1 = 0ull, t2 = 0ull;
+    if (c < n) {
+#pragma unroll
+      for (int r = 0; r < kHistRep; ++r) {
+        t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
+    sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
+    trace(__builtin_amdgcn_s_memrealtime());
+    return;
+  }
+  unsigned long long* T1v = sumA;                 // reuse LDS: n each
+  unsigned long long* T2v = sumN;
   for (int c = threadIdx.x; c < n; c += blockDim.x) {
     unsigned long long t1 = 0ull, t2 = 0ull;
 #pragma unroll
@@ -820,7 +962,6 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
     T1v[c] = t1; T2v[c] = t2;
   }
   __syncthreads();
-  __shared__ int lsel[2 + kMaxSel];
   if (threadIdx.x < 64) {
     const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
@@ -839,29 +980,41 @@ __global__ __launch_bounds__(512, 4) void k_mse_hist3(const ProbDesc* __restrict
 // iteration for ~10 k elements). Same integers and the same float32 operations as the
 // multi-block path (the histograms are exact sums; S2 only sets the rigorous bounds).
 template <int QMAX, int G>   // G: float4 groups per thread (1024 threads x 4 G elements cover the job)
-__global__ __launch_bounds__(1024) void k_mse_small_admm(const ProbDesc* __restrict__ d, const int* __restrict__ jobs,
+__global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc* __restrict__ d, const int* __restrict__ jobs,
                                                          int ncand, int bits, int slot, int iter,
                                                          const unsigned short* __restrict__ rank0,
                                                          const unsigned short* __restrict__ groups, int ngroups) {
-  const ProbDesc& p = d[jobs[blockIdx.x]];
+  ADMMQ_SMALL_STAMP(0);
+  // the job index through a scalar register: the descriptor fields are then scalar loads
+  const ProbDesc& p = d[__builtin_amdgcn_readfirstlane(jobs[blockIdx.x])];
   const long long total = (long long)p.I * p.ld;
-  // every element of the job is loaded up front (H_T, U for the search; H, F too for the
-  // finalize step): their latency overlaps the threshold-table setup
+  // the stop flag and max|x| first (the table setup needs only them), then every element
+  // of the job (H_T, U for the search; H, F too for the finalize step), straight-line
+  // (past the end a clamped address, zeroed below): the element loads stay in flight
+  // through the threshold-table setup
+  const int stopped = gld_i32(p.flags);
+  const float mx = __uint_as_float(gld_u32(p.mv.stat + 4 * slot));
+  H3Pre pre;
+  h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kSmallThreads);
+  asm volatile("" ::: "memory");   // issue order: the loads above before the element loads
+  const float *HTp = p.HT, *Up = p.U, *Hp = p.H, *Fpp = p.Fp;
   float4 t4[G], u4[G], h4[G], f4[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const long long e = 4LL * threadIdx.x + 4096LL * g;
-    t4[g] = make_float4(0.f, 0.f, 0.f, 0.f); u4[g] = t4[g]; h4[g] = t4[g]; f4[g] = t4[g];
-    if (e < total) {
-      t4[g] = *reinterpret_cast<const float4*>(p.HT + e);
-      u4[g] = *reinterpret_cast<const float4*>(p.U + e);
-      h4[g] = *reinterpret_cast<const float4*>(p.H + e);
-      f4[g] = *reinterpret_cast<const float4*>(p.Fp + e);
-    }
+    const long long ec = e < total ? e : 0;
+    t4[g] = gld4(HTp + ec);
+    u4[g] = gld4(Up + ec);
   }
-  if (p.flags[0]) return;   // converged earlier (sticky break)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const long long e = 4LL * threadIdx.x + 4096LL * g;
+    const long long ec = e < total ? e : 0;
+    h4[g] = gld4(Hp + ec);
+    f4[g] = gld4(Fpp + ec);
+  }
   const MseView& v = p.mv;
-  const float mx = __uint_as_float(v.stat[4 * slot]);
+  ADMMQ_SMALL_STAMP(1);
   int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long wtot[16], wtot2[16];
@@ -881,40 +1034,44 @@ __global__ __launch_bounds__(1024) void k_mse_small_admm(const ProbDesc* __restr
     float* tsort = thr + M;
     unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);
     unsigned short* cell = rnk + ((M + 1) & ~1);
-    const float inv = h3_setup<QMAX>(mx, n, rank0, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell);
+    const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell, kSmallThreads);
+    // the stop test after the (LDS-only) setup: tested earlier, the compiler would sink
+    // the element loads below it and their latency would no longer overlap the setup
+    if (stopped) return;   // converged earlier (sticky break)
+    ADMMQ_SMALL_STAMP(2);
     const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
     const int dummy = M + 1 + lane;
+#pragma unroll
+    for (int g = 0; g < G; ++g)   // past the end: zeros (the clamped loads read element 0)
+      if (4LL * threadIdx.x + 4096LL * g >= total) { t4[g] = make_float4(0.f, 0.f, 0.f, 0.f); u4[g] = t4[g]; }
     double s2 = 0.0;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const float xs[4] = {t4[g].x - u4[g].x, t4[g].y - u4[g].y, t4[g].z - u4[g].z, t4[g].w - u4[g].w};   // H_T - U
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        s2 += (double)xs[k] * (double)xs[k];
-        h3_insert(xs[k], inv, tsort, cell, K1, dummy, sumA, sumN, cntA, cntN);
-      }
+      for (int k = 0; k < 4; ++k) s2 += (double)xs[k] * (double)xs[k];
+      h3_insert_n<4>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
     }
     __syncthreads();
-    h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
+    ADMMQ_SMALL_STAMP(3);
+    h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b, kSmallThreads);
+    ADMMQ_SMALL_STAMP(4);
     unsigned long long t1 = 0ull, t2 = 0ull;   // candidate tid (n <= 1024)
     if ((int)threadIdx.x < n) h3_totals<QMAX>(threadIdx.x, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
     if (lane == 0) red[w] = s2;
-    __syncthreads();   // every thread is done with the buckets: T1/T2 go where they were
-    unsigned long long* T1v = sumA;
-    unsigned long long* T2v = sumN;
-    if ((int)threadIdx.x < n) { T1v[threadIdx.x] = t1; T2v[threadIdx.x] = t2; }
     __syncthreads();
-    if (threadIdx.x < 64) {
-      double S2 = 0.0;
-      for (int k = 0; k < nw; ++k) S2 += red[k];
-      select_wave2(v, sel, lsel, T1v, T2v, S2, mx, n, QMAX);
-    }
-    __syncthreads();
+    double S2 = 0.0;
+    for (int k = 0; k < nw; ++k) S2 += red[k];
+    select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
+    ADMMQ_SMALL_STAMP(5);
+    if (threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][8] = (unsigned)lsel[0];
     sse_in_block(v, lsel, n, bits, slot, mx, reinterpret_cast<float4*>(smem));
     __syncthreads();
+    ADMMQ_SMALL_STAMP(6);
   }
+  if (stopped) return;   // (degenerate max|x|: no setup above)
   // k_finalize_admm's step (source/admm.py:59-65) with the chosen scale
   const QParams qp = block_qparams(kMse, bits, v, slot, ncand, 0, 0.f, 0.f);
   const float rho = p.rho[0];
@@ -968,6 +1125,7 @@ __global__ __launch_bounds__(1024) void k_mse_small_admm(const ProbDesc* __restr
     double* rs = p.res + 4 * kResRep * (slot ^ 1);
     for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
   }
+  ADMMQ_SMALL_STAMP(7);
 }
 
 // maxtotal: the largest I * ld among the jobs (picks G); 0 when the path cannot run
@@ -982,7 +1140,7 @@ void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ng
   if (njobs <= 0) return;
   const size_t lds = hist3_lds_bytes(ncand, bits);
 #define ADMMQ_SMG(Q, GG) \
-  hipLaunchKernelGGL((k_mse_small_admm<Q, GG>), dim3(njobs), dim3(1024), lds, s, d, jobs, ncand, bits, slot, iter, \
+  hipLaunchKernelGGL((k_mse_small_admm<Q, GG>), dim3(njobs), dim3(kSmallThreads), lds, s, d, jobs, ncand, bits, slot, iter, \
                      rank0, groups, ngroups)
 #define ADMMQ_SM(Q)                        \
   switch (ngr) {                           \
@@ -1105,7 +1263,7 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
   if (nchunks <= 0) return;
   const size_t lds = hist3_lds_bytes(ncand, bits);
 #define ADMMQ_H3(Q, V)                                                                                        \
-  hipLaunchKernelGGL((k_mse_hist3<Q, V>), dim3(nchunks), dim3(512), lds, s, d, q, chunks, ncand, slot, rank0, \
+  hipLaunchKernelGGL((k_mse_hist3<Q, V>), dim3(nchunks), dim3(kH3Threads), lds, s, d, q, chunks, ncand, slot, rank0, \
                      groups, ngroups)
 #define ADMMQ_H3N(Q) if (nv == 2) ADMMQ_H3(Q, 2); else ADMMQ_H3(Q, 1)
   switch (bits) {

@@ -147,7 +147,7 @@ struct AdmmPlan {
   Chunk* d_hist = nullptr;
   unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
   int nsplit = 0;                // split-K tile pairs
-  float* d_kpart = nullptr;      // [nsplit][2][64 x 64] partial sums
+  float* d_kpart = nullptr;      // [nsplit][2][(32 WM) x 64] partial sums (big tiles)
   unsigned* d_pcnt = nullptr;    // [nsplit] arrival counters (zeroed per run)
   std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
   ThinUnit* d_thin = nullptr;
@@ -421,7 +421,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
   pl.d_queue = cv.take<unsigned>(2);
-  pl.d_kpart = cv.take<float>((size_t)std::max(pl.nsplit, 1) * 2 * 64 * 64);
+  pl.d_kpart = cv.take<float>((size_t)std::max(pl.nsplit, 1) * 2 * (32 * gemm_big_wm()) * 64);
   pl.d_pcnt = cv.take<unsigned>(std::max(pl.nsplit, 1));
   pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
   pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));

@@ -97,7 +97,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // chain over its 1/KS slice of the k range of every K-step; the partials are summed in
 // fixed order at the end.
 template <int WM, int KS, int NS, int NA = 1>   // NA: independent accumulator chains per wave (1 or 2)
-__global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
+__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? 3 : 1))) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
                                                         int ntiles, unsigned* __restrict__ queue,
                                                         float* __restrict__ kpart, unsigned* __restrict__ pcnt, int slot,
                                                         int iter, float eps, int ncand) {
@@ -146,6 +146,19 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
     const int ld = p.ld, ldm = p.ldm;
     const int row0 = tl.tm * BM, col0 = tl.tn * BN;
     const int nk = tl.nk;
+    // the epilogue's U entries (X = H_T - U), loaded before the first stages so their
+    // latency is spent under the K-loop, not after it (vector loads complete in issue
+    // order: the stage waits below then also cover these)
+    float upre[16];
+    {
+      const int col = col0 + 32 * wn + i;
+      const int colc = col < ld ? col : 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+        upre[r] = ldg(p.U + (size_t)row * ld + colc);
+      }
+    }
     // per-lane global source of each of this wave's glds pieces (K-step 0)
     const float* src[GPW];
 #pragma unroll
@@ -283,7 +296,7 @@ __global__ __launch_bounds__(128 * WM * KS) void k_gemm(const ProbDesc* __restri
             const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
             const size_t off = (size_t)row * ld + col;
             const float ht = acc[r];
-            const float x = ht - p.U[off];
+            const float x = ht - upre[r];
             p.HT[off] = ht;
             if (p.X_dbg) p.X[off] = x;   // X = H_T - U is re-formed by its readers; stored for debug output only
             if (row < p.I && col < p.R) {

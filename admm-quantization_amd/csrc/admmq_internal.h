@@ -90,7 +90,13 @@ struct QJob {
 // Work-unit tables (built on the host, uploaded once per call)
 // GEMM tile: rows tm, columns tn of problem prob, K-steps [k0, k0 + nk). part >= 0: one
 // half (ks = 0 / 1) of a split-K pair, whose second-arriving half finishes the tile.
-struct GemmTile { int prob, tm, tn, first, k0, nk, part, ks; };
+// The operands' addresses and strides ride along (filled at upload), so a tile's first
+// loads depend on the tile entry only, not on a further descriptor read.
+struct GemmTile {
+  int prob, tm, tn, first, k0, nk, part, ks;
+  const float* P; const float* M; const float* U;
+  int ld, ldm;
+};
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
 struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
 // Work unit {job, first element}. Stage-1 units also carry the job's inputs that the

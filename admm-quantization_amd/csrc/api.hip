@@ -176,6 +176,7 @@ static bool thin_enabled() {
 static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
   GemmTile t;
   t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.k0 = 0; t.nk = nk; t.part = -1; t.ks = 0;
+  t.P = nullptr; t.M = nullptr; t.U = nullptr; t.ld = 0; t.ldm = 0;   // set at upload
   return t;
 }
 
@@ -436,6 +437,10 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
 static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   int rc;
   if ((rc = h2d(pl.d_desc, pl.desc.data(), pl.desc.size() * sizeof(ProbDesc), s))) return rc;
+  for (GemmTile& t : pl.tiles) {
+    const ProbDesc& d = pl.desc[t.prob];
+    t.P = d.P; t.M = d.M; t.U = d.U; t.ld = d.ld; t.ldm = d.ldm;
+  }
   if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;

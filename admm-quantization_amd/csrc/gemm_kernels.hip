@@ -143,7 +143,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
     const unsigned long long t_tile = __builtin_amdgcn_s_memrealtime();
     const GemmTile tl = tiles[t];
     const ProbDesc& p = probs[tl.prob];
-    const int ld = p.ld, ldm = p.ldm;
+    const int ld = tl.ld, ldm = tl.ldm;
     const int row0 = tl.tm * BM, col0 = tl.tn * BN;
     const int nk = tl.nk;
     // the epilogue's U entries (X = H_T - U), loaded before the first stages so their
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-        upre[r] = ldg(p.U + (size_t)row * ld + colc);
+        upre[r] = ldg(tl.U + (size_t)row * ld + colc);
       }
     }
     // per-lane global source of each of this wave's glds pieces (K-step 0)
@@ -166,8 +166,8 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
       const int g = wave * GPW + j;
       const int r = 8 * g + (lane >> 3);                       // image row
       const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
-      src[j] = (r < BM) ? p.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
-                        : p.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
+      src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
+                        : tl.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
     }
 #define ADMMQ_ISSUE(s, kt)                                                 \
   _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \

@@ -69,24 +69,24 @@ template <int G>   // float4 groups per thread: 256 G * 4 elements per work unit
 __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restrict__ probs, const Chunk* __restrict__ chunks,
                                                        int ncand, int bits, int scheme, int slot, int iter) {
   const Chunk ck = chunks[blockIdx.x];
-  const ProbDesc& p = probs[ck.job];
-  const long long total = (long long)p.I * p.ld;
-  // float4 group g of thread t at start + 4 t + 1024 g. Element loads first: independent
-  // of the quantizer parameters and of the stop flag, so their latency overlaps the
-  // parameter chain (stat -> sel -> sse) and the flag read below.
+  // float4 group g of thread t at start + 4 t + 1024 g. The stop flag, then the element
+  // loads, straight from the unit (no descriptor read first; past the end a clamped
+  // address, never used): independent of the quantizer parameters, so their latency
+  // overlaps the parameter chain (descriptor -> stat -> sel -> sse) below.
+  const long long total = ck.total;
+  const int stopped = gld_i32(ck.done);
   float4 t4[G], h4[G], u4[G], f4[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
-    t4[g] = make_float4(0.f, 0.f, 0.f, 0.f); h4[g] = t4[g]; u4[g] = t4[g]; f4[g] = t4[g];
-    if (e < total) {
-      t4[g] = *reinterpret_cast<const float4*>(p.HT + e);
-      h4[g] = *reinterpret_cast<const float4*>(p.H + e);
-      u4[g] = *reinterpret_cast<const float4*>(p.U + e);
-      f4[g] = *reinterpret_cast<const float4*>(p.Fp + e);
-    }
+    const long long ec = e < total ? e : 0;
+    t4[g] = gld4(ck.X + ec);
+    h4[g] = gld4(ck.H + ec);
+    u4[g] = gld4(ck.U + ec);
+    f4[g] = gld4(ck.F + ec);
   }
-  if (p.flags[0]) return;   // converged earlier (sticky break)
+  const ProbDesc& p = probs[ck.job];
+  if (stopped) return;   // converged earlier (sticky break)
   const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);
   const float rho = p.rho[0];
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;

@@ -109,6 +109,8 @@ struct Chunk {
   const float* X;
   const float* U;   // non-null: the element is X - U (ADMM: H_T - U)
   long long total;
+  const float* H;   // ADMM finalize units: the current H and the padded F
+  const float* F;
 };
 
 // Loads through global (not flat) pointers: flat loads also count in lgkmcnt, and a

@@ -405,7 +405,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       if (pass == 1) pl.small.push_back(i);
       for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
       const long long tot = (long long)d.I * d.ld;
-      for (long long e = 0; e < tot; e += pl.fin_elems) pl.fin_chunks.push_back({i, (int)e});
+      for (long long e = 0; e < tot; e += pl.fin_elems)
+        pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot, d.H, d.Fp});
       const long long hu = (long long)kHistElems * pl.hist_nv;
       for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
       pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);

@@ -656,17 +656,22 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
   const int M = QMAX * n;
   const int nb = M + 1 + 64;
   ADMMQ_SETUP_STAMP(0);
-  fill_thresholds(thr, mx, n, QMAX, nt);   // overlaps the latency of the order (and element) loads
+  // thresholds, each also scattered to its host-order rank (kR0 * nt >= kMaxMerged >= M)
+  const float den = (float)(2 * QMAX - 1);
 #pragma unroll
   for (int j = 0; j < kR0; ++j) {
-    const int i = threadIdx.x + j * nt;
-    if (i < M) rnk[i] = pre.r0v[j];
+    const int e = threadIdx.x + j * nt;
+    if (e < M) {
+      const int k = 1 + e / n, c = e - (k - 1) * n;
+      const float v = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
+      thr[e] = v;
+      tsort[pre.r0v[j]] = v;
+      rnk[e] = pre.r0v[j];
+    }
   }
   for (int i = threadIdx.x; i < nb; i += nt) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
   __syncthreads();
   ADMMQ_SETUP_STAMP(1);
-  for (int e = threadIdx.x; e < M; e += nt) tsort[rnk[e]] = thr[e];
-  __syncthreads();
   // exact-key ties: order by actual value (the thread's first group was prefetched; a
   // load in the same loop would, after the join, make the compiler wait for every
   // outstanding load, the elements included)
@@ -692,31 +697,39 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
     for (int g = threadIdx.x + nt; g < ngroups; g += nt) tie_group(groups + 6 * g);
   __syncthreads();
   ADMMQ_SETUP_STAMP(2);
+  // one pass over the sorted table: the order check, L = 1 + index of the last equal
+  // value, and the coarse index cell(v) = min(kCells-1, (int)(v * inv)) (non-decreasing
+  // in v, so thresholds in cells below cell(a) are < a and those above are > a)
+  const float inv = (float)kCells / tsort[M - 1];
+  auto fill_cells = [&](float iv) {
+    for (int r = threadIdx.x; r < M; r += nt) {
+      const int cr = min(kCells - 1, (int)(tsort[r] * iv));
+      const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * iv));
+      for (int g = cp + 1; g <= cr; ++g) cell[g] = (unsigned short)r;
+      if (r == M - 1)
+        for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
+    }
+  };
   int bad = 0;
   for (int r = threadIdx.x; r + 1 < M; r += nt) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
-  if (__syncthreads_or(bad)) {
-    rank_by_counting(thr, tsort, rnk, mx, n, QMAX);   // never expected; exact either way
-  } else {
-    for (int e = threadIdx.x; e < M; e += nt) {   // L = 1 + index of the last equal value
-      const int r = rnk[e];
-      int l = r + 1;
-      while (l < M && tsort[l] == tsort[r]) ++l;
-      rnk[e] = (unsigned short)l;
-    }
+  for (int e = threadIdx.x; e < M; e += nt) {
+    const int r = rnk[e];
+    int l = r + 1;
+    while (l < M && tsort[l] == tsort[r]) ++l;
+    rnk[e] = (unsigned short)l;
   }
-  __syncthreads();
+  fill_cells(inv);
+  if (__syncthreads_or(bad)) {   // never expected: rank by counting, then the cells again (exact either way)
+    rank_by_counting(thr, tsort, rnk, mx, n, QMAX);
+    __syncthreads();
+    const float inv2 = (float)kCells / tsort[M - 1];
+    fill_cells(inv2);
+    __syncthreads();
+    ADMMQ_SETUP_STAMP(3);
+    ADMMQ_SETUP_STAMP(4);
+    return inv2;
+  }
   ADMMQ_SETUP_STAMP(3);
-  // coarse index: cell(v) = min(kCells-1, (int)(v * inv)) is non-decreasing in v, so
-  // thresholds in cells below cell(a) are < a and those above are > a
-  const float inv = (float)kCells / tsort[M - 1];
-  for (int r = threadIdx.x; r < M; r += nt) {
-    const int cr = min(kCells - 1, (int)(tsort[r] * inv));
-    const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * inv));
-    for (int g = cp + 1; g <= cr; ++g) cell[g] = (unsigned short)r;
-    if (r == M - 1)
-      for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
-  }
-  __syncthreads();
   ADMMQ_SETUP_STAMP(4);
   return inv;
 }

@@ -33,7 +33,7 @@ n = 4096
 buf = (ctypes.c_ulonglong * (5 * n))()
 got = fn(buf, n)
 rows = [[buf[5 * b + k] for k in range(5)] for b in range(got) if buf[5 * b] and buf[5 * b + 4] >= buf[5 * b]]
-names = ["thresholds+order", "scatter+ties", "sorted check+L", "cells"]
+names = ["thresholds+scatter", "ties", "check+L+cells", "(fallback)"]
 print(f"blocks {len(rows)}")
 for k, nm in enumerate(names):
     d = [(r[k + 1] - r[k]) / 100 for r in rows]

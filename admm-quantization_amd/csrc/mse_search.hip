@@ -778,22 +778,79 @@ __device__ __forceinline__ void h3_insert_n(const float* xs, float inv, const fl
 
 // all = positives + negatives, then suffix sums S[i] = sum over buckets >= i of the four
 // bucket arrays in one block pass: contiguous per-thread runs, then a scan of the run
-// totals over the block (in thread order). Ends with a block barrier.
+// totals over the block (in thread order; the wave totals are summed by an unrolled,
+// predicated loop, so their reads are issued together). Runs of up to PMAX buckets are
+// held in registers (one round of independent LDS reads, one of writes); longer ones
+// are walked in LDS. PMAX = 0: the walk in LDS and a plain loop over the wave totals
+// (fewest registers). Ends with a block barrier.
+template <int NT, int PMAX>
 __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
                                           unsigned* cntN, unsigned long long* wtot, unsigned long long* wtot2,
-                                          unsigned* wtot32, unsigned* wtot32b, int nt) {
+                                          unsigned* wtot32, unsigned* wtot32b) {
+  constexpr int NW = NT / 64;
   const int len = M + 1;
-  const int per = (len + nt - 1) / nt;
+  const int per = (len + NT - 1) / NT;
   const int b0 = threadIdx.x * per, b1 = min(b0 + per, len);
+  if constexpr (PMAX == 0) {   // fewest registers (the 1024-thread kernel holds its elements across this)
+    unsigned long long r1 = 0ull, r2 = 0ull;
+    unsigned r3 = 0u, r4 = 0u;
+    for (int i = b1 - 1; i >= b0; --i) {
+      const unsigned long long sn = sumN[i];
+      const unsigned c = cntN[i];
+      r1 += sumA[i] + sn; sumA[i] = r1;
+      r2 += sn; sumN[i] = r2;
+      r3 += cntA[i] + c; cntA[i] = r3;
+      r4 += c; cntN[i] = r4;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long q1 = r1, q2 = r2;
+    unsigned q3 = r3, q4 = r4;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
+      const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
+      if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
+    }
+    if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
+    __syncthreads();
+    unsigned long long a1 = 0ull, a2 = 0ull;
+    unsigned a3 = 0u, a4 = 0u;
+    for (int j = w + 1; j < NW; ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
+    const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
+    const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
+    if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
+    for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
+    __syncthreads();
+    return;
+  }
+  constexpr int PM = PMAX > 0 ? PMAX : 1;
+  const bool inreg = per <= PMAX;   // block-uniform
+  unsigned long long ra[PM], rn[PM];
+  unsigned ca[PM], cn[PM];
   unsigned long long r1 = 0ull, r2 = 0ull;
   unsigned r3 = 0u, r4 = 0u;
-  for (int i = b1 - 1; i >= b0; --i) {   // the thread's own run: all = positives + negatives here
-    const unsigned long long sn = sumN[i];
-    const unsigned cn = cntN[i];
-    r1 += sumA[i] + sn; sumA[i] = r1;
-    r2 += sn; sumN[i] = r2;
-    r3 += cntA[i] + cn; cntA[i] = r3;
-    r4 += cn; cntN[i] = r4;
+  if (inreg) {
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const int idx = b0 + i;
+      const bool ok = idx < b1;
+      ra[i] = ok ? sumA[idx] : 0ull; rn[i] = ok ? sumN[idx] : 0ull;
+      ca[i] = ok ? cntA[idx] : 0u;   cn[i] = ok ? cntN[idx] : 0u;
+    }
+#pragma unroll
+    for (int i = PM - 1; i >= 0; --i) {   // entries past the run are zero
+      r1 += ra[i] + rn[i]; r2 += rn[i]; r3 += ca[i] + cn[i]; r4 += cn[i];
+      ra[i] = r1; rn[i] = r2; ca[i] = r3; cn[i] = r4;
+    }
+  } else {
+    for (int i = b1 - 1; i >= b0; --i) {
+      const unsigned long long sn = sumN[i];
+      const unsigned c = cntN[i];
+      r1 += sumA[i] + sn; sumA[i] = r1;
+      r2 += sn; sumN[i] = r2;
+      r3 += cntA[i] + c; cntA[i] = r3;
+      r4 += c; cntN[i] = r4;
+    }
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned long long q1 = r1, q2 = r2;
@@ -805,14 +862,24 @@ __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsig
     if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
   }
   if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
+  const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
+  const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
   __syncthreads();
   unsigned long long a1 = 0ull, a2 = 0ull;
   unsigned a3 = 0u, a4 = 0u;
-  for (int j = w + 1; j < (nt >> 6); ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
-  const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
-  const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
+#pragma unroll
+  for (int j = 1; j < NW; ++j)
+    if (j > w) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
   if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
-  for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
+  if (inreg) {
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const int idx = b0 + i;
+      if (idx < b1) { sumA[idx] = ra[i] + a1; sumN[idx] = rn[i] + a2; cntA[idx] = ca[i] + a3; cntN[idx] = cn[i] + a4; }
+    }
+  } else {
+    for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
+  }
   __syncthreads();
 }
 
@@ -906,7 +973,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   }
   __syncthreads();
   const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
-  h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b, kH3Threads);
+  h3_suffix<kH3Threads, 4>(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
   // per-candidate totals of this block into one of kHistRep replicas
   const int rep = blockIdx.x & (kHistRep - 1);
   unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
@@ -1067,7 +1134,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
     }
     __syncthreads();
     ADMMQ_SMALL_STAMP(3);
-    h3_suffix(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b, kSmallThreads);
+    h3_suffix<kSmallThreads, 0>(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
     ADMMQ_SMALL_STAMP(4);
     unsigned long long t1 = 0ull, t2 = 0ull;   // candidate tid (n <= 1024)
     if ((int)threadIdx.x < n) h3_totals<QMAX>(threadIdx.x, n, rnk, sumA, sumN, cntA, cntN, t1, t2);

@@ -71,18 +71,23 @@ __device__ void chol32(double* a, int* err) {
   __syncthreads();
 }
 
-// Inverse of a lower-triangular 32x32 block: column c by thread c.
+// Inverse of a lower-triangular 32x32 block: column c by thread c, held in registers
+// (fully unrolled: the LDS reads of l are broadcasts with no dependence on the chain,
+// so they issue ahead; only the fp64 FMA chain of each row is serial).
 __device__ void trinv32(const double* l, double* x) {
-  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) x[(t >> 5) * LS + (t & 31)] = 0.0;
-  __syncthreads();
   if (threadIdx.x < NB) {
     const int c = threadIdx.x;
-    x[c * LS + c] = 1.0 / l[c * LS + c];
-    for (int r = c + 1; r < NB; ++r) {
+    double col[NB];
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
       double s = 0.0;
-      for (int t = c; t < r; ++t) s += l[r * LS + t] * x[t * LS + c];
-      x[r * LS + c] = -s / l[r * LS + r];
+#pragma unroll
+      for (int t = 0; t < r; ++t) s += l[r * LS + t] * col[t];   // col[t] = 0 for t < c
+      const double d = l[r * LS + r];
+      col[r] = r < c ? 0.0 : (r == c ? 1.0 / d : -s / d);
     }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) x[r * LS + c] = col[r];
   }
   __syncthreads();
 }
@@ -203,6 +208,76 @@ __global__ __launch_bounds__(256) void k_linv_row(const ProbDesc* __restrict__ p
   store_block(p.L64, p.ldm, i, j, tb);
 }
 
+// Diagonal blocks of Linv: Linv_ii = L_ii^-1, all i of all problems in one launch.
+__global__ __launch_bounds__(256) void k_diag_inv(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  const int i = blockIdx.x;
+  if (i >= p.nbk) return;
+  __shared__ double lii[NB * LS], xi[NB * LS];
+  load_block(lii, p.D64, NB, i, 0);
+  __syncthreads();
+  trinv32(lii, xi);
+  store_block(p.L64, p.ldm, i, i, xi);
+}
+
+// Off-diagonal blocks of Linv by column slices: the columns of Linv are independent
+// forward substitutions, so one workgroup owns a 4-column slice of block column j and
+// walks down the block rows i = j+1 .. nbk-1 with its finished rows kept in LDS:
+//   Linv_ij = -Linv_ii sum_{t=j}^{i-1} L_it Linv_tj
+// One launch replaces the nbk dependent row launches. Thread (r, c) owns output row r,
+// column c of the slice; L_it rows are read straight from global (4 threads share a
+// row), the slice's earlier blocks from LDS. Four partial sums per thread (k mod 4)
+// keep four independent fp64 FMA chains.
+constexpr int kLinvCols = 4;
+constexpr int kLinvMaxNbk = 56;   // LDS panel: nbk x 32 x 4 doubles (56 KB at the cap)
+__global__ __launch_bounds__(128) void k_linv_cols(const ProbDesc* __restrict__ probs) {
+  const ProbDesc& p = probs[blockIdx.y];
+  constexpr int nsl = NB / kLinvCols;
+  const int j = blockIdx.x / nsl, c0 = (blockIdx.x % nsl) * kLinvCols;
+  const int nbk = p.nbk, ldm = p.ldm;
+  if (j >= nbk - 1) return;
+  // dynamic LDS: panel [maxnbk][32][4] (block rows t >= j used), then sbuf [32][4]
+  extern __shared__ double linv_lds[];
+  double* panel = linv_lds;
+  double* sbuf = linv_lds + (size_t)(gridDim.x / nsl + 1) * NB * kLinvCols;
+  const int r = threadIdx.x >> 2, c = threadIdx.x & 3;
+  const double* A64 = p.A64;
+  double* L64 = p.L64;
+  // block (j, j) slice: Linv_jj, written by k_diag_inv
+  panel[(j * NB + r) * kLinvCols + c] = L64[(size_t)(j * NB + r) * ldm + j * NB + c0 + c];
+  __syncthreads();
+  for (int i = j + 1; i < nbk; ++i) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const double* lrow = A64 + (size_t)(i * NB + r) * ldm;
+    for (int t = j; t < i; ++t) {
+      const double2* lp = reinterpret_cast<const double2*>(lrow + t * NB);
+      const double* pt = panel + t * NB * kLinvCols + c;
+#pragma unroll
+      for (int k = 0; k < NB; k += 4) {
+        const double2 x0 = lp[k / 2], x1 = lp[k / 2 + 1];
+        a0 += x0.x * pt[(k + 0) * kLinvCols];
+        a1 += x0.y * pt[(k + 1) * kLinvCols];
+        a2 += x1.x * pt[(k + 2) * kLinvCols];
+        a3 += x1.y * pt[(k + 3) * kLinvCols];
+      }
+    }
+    sbuf[r * kLinvCols + c] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    const double2* dp = reinterpret_cast<const double2*>(L64 + (size_t)(i * NB + r) * ldm + i * NB);
+    double o0 = 0.0, o1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; k += 2) {
+      const double2 d = dp[k / 2];
+      o0 += d.x * sbuf[k * kLinvCols + c];
+      o1 += d.y * sbuf[(k + 1) * kLinvCols + c];
+    }
+    const double o = -(o0 + o1);
+    panel[(i * NB + r) * kLinvCols + c] = o;
+    L64[(size_t)(i * NB + r) * ldm + j * NB + c0 + c] = o;
+    __syncthreads();   // sbuf is rewritten and block i is read by every thread next step
+  }
+}
+
 __global__ __launch_bounds__(256) void k_minv(const ProbDesc* __restrict__ probs) {
   const ProbDesc& p = probs[blockIdx.y];
   const int q = blockIdx.x;
@@ -242,7 +317,14 @@ void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s)
     const int n = maxnbk - k - 1;
     if (n > 0) hipLaunchKernelGGL(k_chol_update, dim3(n * (n + 1) / 2, nprob), dim3(256), 0, s, d, k);
   }
-  for (int i = 0; i < maxnbk; ++i) hipLaunchKernelGGL(k_linv_row, dim3(i + 1, nprob), dim3(256), 0, s, d, i);
+  if (maxnbk <= kLinvMaxNbk) {
+    hipLaunchKernelGGL(k_diag_inv, dim3(maxnbk, nprob), dim3(256), 0, s, d);
+    if (maxnbk > 1)
+      hipLaunchKernelGGL(k_linv_cols, dim3((maxnbk - 1) * (NB / kLinvCols), nprob), dim3(128),
+                         (size_t)(maxnbk + 1) * NB * kLinvCols * sizeof(double), s, d);
+  } else {   // panel would not fit in LDS: one launch per block row
+    for (int i = 0; i < maxnbk; ++i) hipLaunchKernelGGL(k_linv_row, dim3(i + 1, nprob), dim3(256), 0, s, d, i);
+  }
   hipLaunchKernelGGL(k_minv, dim3(maxnbk * (maxnbk + 1) / 2, nprob), dim3(256), 0, s, d);
 }
 

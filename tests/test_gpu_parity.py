@@ -227,6 +227,28 @@ def test_thin_factor_solve(torch_dev, I, R):
         assert _rel(HT.cpu().numpy(), info["HT"]) < 1e-5
 
 
+@pytest.mark.parametrize("R", [33, 1790, 1830])
+def test_spd_inverse_paths(torch_dev, R):
+    """The SPD inverse: R <= 1792 (56 blocks of 32) takes the one-launch column-slice
+    Linv (k_diag_inv + k_linv_cols), larger R the per-block-row launches (k_linv_row).
+    One step vs the oracle, batched with a small problem of a different block count."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    rng = np.random.default_rng(R)
+    probs, ref = [], []
+    for (i, r) in [(48, R), (20, 70)]:
+        B = rng.standard_normal((r, 2 * r)).astype(np.float32) / np.float32(np.sqrt(2 * r))
+        G = (B @ B.T + 0.5 * np.eye(r)).astype(np.float32)
+        F = rng.standard_normal((i, r)).astype(np.float32)
+        H0 = (rng.standard_normal((i, r)) * 0.1).astype(np.float32)
+        U0 = (rng.standard_normal((i, r)) * 0.01).astype(np.float32)
+        probs.append((_t(torch, dev, H0), _t(torch, dev, U0), _t(torch, dev, F), _t(torch, dev, G)))
+        ref.append(ao.admm_iteration(H0, U0, F, G, 2, 1e-8, 4, MSE, return_info=True)[2])
+    Hs, dbg = admm_iteration_batched(probs, 2, 1e-8, 4, MSE, debug_outputs=True)
+    for (HT, X), info in zip(dbg, ref):
+        assert _rel(HT.cpu().numpy(), info["HT"]) < 1e-5
+
+
 # ----------------------------------------------------------------------------- P3
 def test_batched_equals_single_and_deterministic(torch_dev):
     torch, dev = torch_dev

@@ -16,11 +16,13 @@ namespace admmq {
 constexpr int NB = 32;
 constexpr int LS = NB + 1;  // LDS row stride (doubles) to spread banks
 
+__device__ __forceinline__ void load_regs(double r[4], const double* A, int ldm, int bi, int bj);
+__device__ __forceinline__ void store_regs(double* dst, const double r[4]);
+// blocks of 256 threads: all four loads of a thread issue before the first LDS store
 __device__ __forceinline__ void load_block(double* dst, const double* A, int ldm, int bi, int bj) {
-  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
-    const int r = t >> 5, c = t & 31;
-    dst[r * LS + c] = A[(size_t)(bi * NB + r) * ldm + bj * NB + c];
-  }
+  double r[4];
+  load_regs(r, A, ldm, bi, bj);
+  store_regs(dst, r);
 }
 __device__ __forceinline__ void store_block(double* A, int ldm, int bi, int bj, const double* src) {
   for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
@@ -46,45 +48,58 @@ __device__ __forceinline__ void store_regs(double* dst, const double r[4]) {
   }
 }
 
-// In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed. One wave: lane r
+// holds row r in registers; the pivot and the column entries l[s][c] are broadcast by
+// readlane, so the 32 right-looking steps need no workgroup barrier.
 __device__ void chol32(double* a, int* err) {
-  for (int c = 0; c < NB; ++c) {
-    if (threadIdx.x == 0) {
-      const double d = a[c * LS + c];
-      if (!(d > 0.0)) *err = 1;
-      a[c * LS + c] = sqrt(d);
+  if (threadIdx.x < NB) {
+    const int r = threadIdx.x;
+    double row[NB];
+#pragma unroll
+    for (int s = 0; s < NB; ++s) row[s] = a[r * LS + s];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      const double d = readlane_d(row[c], c);
+      if (r == 0 && !(d > 0.0)) *err = 1;
+      const double sd = sqrt(d);
+      const double l = r > c ? row[c] / sd : (r == c ? sd : 0.0);
+      row[c] = l;
+#pragma unroll
+      for (int s = c + 1; s < NB; ++s) row[s] -= l * readlane_d(l, s);   // lanes r < s: upper, zeroed below
     }
-    __syncthreads();
-    if (threadIdx.x > c && threadIdx.x < NB) a[threadIdx.x * LS + c] /= a[c * LS + c];
-    __syncthreads();
-    const int n = NB - c - 1;
-    for (int t = threadIdx.x; t < n * n; t += blockDim.x) {
-      const int r = c + 1 + t / n, s = c + 1 + t % n;
-      if (s <= r) a[r * LS + s] -= a[r * LS + c] * a[s * LS + c];
-    }
-    __syncthreads();
-  }
-  for (int t = threadIdx.x; t < NB * NB; t += blockDim.x) {
-    const int r = t >> 5, c = t & 31;
-    if (c > r) a[r * LS + c] = 0.0;
+#pragma unroll
+    for (int s = 0; s < NB; ++s) a[r * LS + s] = s <= r ? row[s] : 0.0;
   }
   __syncthreads();
 }
 
 // Inverse of a lower-triangular 32x32 block: column c by thread c, held in registers
 // (fully unrolled: the LDS reads of l are broadcasts with no dependence on the chain,
-// so they issue ahead; only the fp64 FMA chain of each row is serial).
+// so they issue ahead). Reciprocal pivots are formed first, off the chain, and each
+// row's sum runs as two interleaved FMA chains.
 __device__ void trinv32(const double* l, double* x) {
   if (threadIdx.x < NB) {
     const int c = threadIdx.x;
-    double col[NB];
+    double rinv[NB], col[NB];
+#pragma unroll
+    for (int r = 0; r < NB; ++r) rinv[r] = 1.0 / l[r * LS + r];
 #pragma unroll
     for (int r = 0; r < NB; ++r) {
-      double s = 0.0;
+      double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-      for (int t = 0; t < r; ++t) s += l[r * LS + t] * col[t];   // col[t] = 0 for t < c
-      const double d = l[r * LS + r];
-      col[r] = r < c ? 0.0 : (r == c ? 1.0 / d : -s / d);
+      for (int t = 0; t + 1 < r; t += 2) {   // col[t] = 0 for t < c
+        s0 += l[r * LS + t] * col[t];
+        s1 += l[r * LS + t + 1] * col[t + 1];
+      }
+      if (r & 1) s0 += l[r * LS + r - 1] * col[r - 1];
+      col[r] = r < c ? 0.0 : (r == c ? rinv[r] : -(s0 + s1) * rinv[r]);
     }
 #pragma unroll
     for (int r = 0; r < NB; ++r) x[r * LS + c] = col[r];
@@ -126,6 +141,8 @@ __global__ __launch_bounds__(256) void k_chol_panel(const ProbDesc* __restrict__
   __shared__ double lkk[NB * LS], x[NB * LS], aik[NB * LS];
   __shared__ int err;
   if (threadIdx.x == 0) err = 0;
+  double ra[4];                      // A_ik in flight while L_kk is factored and inverted
+  if (i != k) load_regs(ra, p.A64, p.ldm, i, k);
   load_block(lkk, p.A64, p.ldm, k, k);
   __syncthreads();
   chol32(lkk, &err);
@@ -135,7 +152,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const ProbDesc* __restrict__
     return;
   }
   trinv32(lkk, x);                   // x = L_kk^-1
-  load_block(aik, p.A64, p.ldm, i, k);
+  store_regs(aik, ra);
   __syncthreads();
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   mm_nt(aik, x, acc);                // L_ik = A_ik * (L_kk^-1)^T
@@ -222,15 +239,22 @@ __global__ __launch_bounds__(256) void k_diag_inv(const ProbDesc* __restrict__ p
 
 // Off-diagonal blocks of Linv by column slices: the columns of Linv are independent
 // forward substitutions, so one workgroup owns a 4-column slice of block column j and
-// walks down the block rows i = j+1 .. nbk-1 with its finished rows kept in LDS:
-//   Linv_ij = -Linv_ii sum_{t=j}^{i-1} L_it Linv_tj
-// One launch replaces the nbk dependent row launches. Thread (r, c) owns output row r,
-// column c of the slice; L_it rows are read straight from global (4 threads share a
-// row), the slice's earlier blocks from LDS. Four partial sums per thread (k mod 4)
-// keep four independent fp64 FMA chains.
+// produces its blocks i = j+1 .. nbk-1 with the finished ones kept in LDS:
+//   Linv_ij = -Linv_ii S_i,   S_i = sum_{t=j}^{i-1} L_it Linv_tj
+// One launch replaces the nbk dependent row launches. Right-looking: as soon as block t
+// of the slice is final, every pending S_i (i > t) takes its L_it Linv_tj term. The
+// 1024 threads are 8 groups of 128; group g owns the S_i with i = j+1+g (mod 8) in
+// registers (thread (r, c) of a group: row r, slice column c), so per block t the
+// pending products run 8 wide and the serial chain is ~1/8 of the slice's work.
+// Sums run over t, then k, in order (the row-launch order).
 constexpr int kLinvCols = 4;
+constexpr int kLinvGroups = 8;
 constexpr int kLinvMaxNbk = 56;   // LDS panel: nbk x 32 x 4 doubles (56 KB at the cap)
-__global__ __launch_bounds__(128) void k_linv_cols(const ProbDesc* __restrict__ probs) {
+constexpr int kLinvPer = (kLinvMaxNbk + kLinvGroups - 1) / kLinvGroups;
+__global__ __launch_bounds__(1024) void k_linv_cols(const ProbDesc* __restrict__ probs) {
+  // grid ((maxnbk-1) * nsl, nprob). Measured: a j-major grid (every problem's long small-j
+  // slices dispatched together) is 3x slower - the 8 slices of a block column each stream
+  // the same L rows, and all of them at once thrash L2.
   const ProbDesc& p = probs[blockIdx.y];
   constexpr int nsl = NB / kLinvCols;
   const int j = blockIdx.x / nsl, c0 = (blockIdx.x % nsl) * kLinvCols;
@@ -240,41 +264,57 @@ __global__ __launch_bounds__(128) void k_linv_cols(const ProbDesc* __restrict__ 
   extern __shared__ double linv_lds[];
   double* panel = linv_lds;
   double* sbuf = linv_lds + (size_t)(gridDim.x / nsl + 1) * NB * kLinvCols;
-  const int r = threadIdx.x >> 2, c = threadIdx.x & 3;
+  const int g = threadIdx.x >> 7, lt = threadIdx.x & 127;
+  const int r = lt >> 2, c = lt & 3;
   const double* A64 = p.A64;
   double* L64 = p.L64;
-  // block (j, j) slice: Linv_jj, written by k_diag_inv
-  panel[(j * NB + r) * kLinvCols + c] = L64[(size_t)(j * NB + r) * ldm + j * NB + c0 + c];
-  __syncthreads();
-  for (int i = j + 1; i < nbk; ++i) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    const double* lrow = A64 + (size_t)(i * NB + r) * ldm;
-    for (int t = j; t < i; ++t) {
-      const double2* lp = reinterpret_cast<const double2*>(lrow + t * NB);
-      const double* pt = panel + t * NB * kLinvCols + c;
+  if (g == 0)   // block (j, j) of the slice: Linv_jj, written by k_diag_inv
+    panel[(j * NB + r) * kLinvCols + c] = L64[(size_t)(j * NB + r) * ldm + j * NB + c0 + c];
+  double acc[kLinvPer];
 #pragma unroll
-      for (int k = 0; k < NB; k += 4) {
-        const double2 x0 = lp[k / 2], x1 = lp[k / 2 + 1];
-        a0 += x0.x * pt[(k + 0) * kLinvCols];
-        a1 += x0.y * pt[(k + 1) * kLinvCols];
-        a2 += x1.x * pt[(k + 2) * kLinvCols];
-        a3 += x1.y * pt[(k + 3) * kLinvCols];
+  for (int q = 0; q < kLinvPer; ++q) acc[q] = 0.0;
+  __syncthreads();
+  for (int t = j; t < nbk - 1; ++t) {
+    const double* pt = panel + t * NB * kLinvCols + c;
+    // pending S_i of this group, i = j + 1 + g + 8q > t
+#pragma unroll
+    for (int q = 0; q < kLinvPer; ++q) {
+      const int i = j + 1 + g + kLinvGroups * q;
+      if (i > t && i < nbk) {
+        const double2* lp = reinterpret_cast<const double2*>(A64 + (size_t)(i * NB + r) * ldm + t * NB);
+        double a = acc[q];
+#pragma unroll
+        for (int k = 0; k < NB; k += 2) {
+          const double2 x = lp[k / 2];
+          a += x.x * pt[k * kLinvCols];
+          a += x.y * pt[(k + 1) * kLinvCols];
+        }
+        acc[q] = a;
       }
     }
-    sbuf[r * kLinvCols + c] = (a0 + a1) + (a2 + a3);
-    __syncthreads();
-    const double2* dp = reinterpret_cast<const double2*>(L64 + (size_t)(i * NB + r) * ldm + i * NB);
-    double o0 = 0.0, o1 = 0.0;
+    // S_{t+1} is complete: its owner group publishes it, then forms Linv_{t+1, j}
+    const int i = t + 1;
+    const int og = (i - j - 1) % kLinvGroups, oq = (i - j - 1) / kLinvGroups;
+    if (g == og) {
+      double v = 0.0;
 #pragma unroll
-    for (int k = 0; k < NB; k += 2) {
-      const double2 d = dp[k / 2];
-      o0 += d.x * sbuf[k * kLinvCols + c];
-      o1 += d.y * sbuf[(k + 1) * kLinvCols + c];
+      for (int q = 0; q < kLinvPer; ++q) v = q == oq ? acc[q] : v;
+      sbuf[r * kLinvCols + c] = v;
     }
-    const double o = -(o0 + o1);
-    panel[(i * NB + r) * kLinvCols + c] = o;
-    L64[(size_t)(i * NB + r) * ldm + j * NB + c0 + c] = o;
-    __syncthreads();   // sbuf is rewritten and block i is read by every thread next step
+    __syncthreads();
+    if (g == og) {
+      const double2* dp = reinterpret_cast<const double2*>(L64 + (size_t)(i * NB + r) * ldm + i * NB);
+      double o = 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; k += 2) {
+        const double2 d = dp[k / 2];
+        o += d.x * sbuf[k * kLinvCols + c];
+        o += d.y * sbuf[(k + 1) * kLinvCols + c];
+      }
+      panel[(i * NB + r) * kLinvCols + c] = -o;
+      L64[(size_t)(i * NB + r) * ldm + j * NB + c0 + c] = -o;
+    }
+    __syncthreads();   // block i of the panel is read by every group next step; sbuf is rewritten
   }
 }
 
@@ -320,7 +360,7 @@ void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s)
   if (maxnbk <= kLinvMaxNbk) {
     hipLaunchKernelGGL(k_diag_inv, dim3(maxnbk, nprob), dim3(256), 0, s, d);
     if (maxnbk > 1)
-      hipLaunchKernelGGL(k_linv_cols, dim3((maxnbk - 1) * (NB / kLinvCols), nprob), dim3(128),
+      hipLaunchKernelGGL(k_linv_cols, dim3((maxnbk - 1) * (NB / kLinvCols), nprob), dim3(1024),
                          (size_t)(maxnbk + 1) * NB * kLinvCols * sizeof(double), s, d);
   } else {   // panel would not fit in LDS: one launch per block row
     for (int i = 0; i < maxnbk; ++i) hipLaunchKernelGGL(k_linv_row, dim3(i + 1, nprob), dim3(256), 0, s, d, i);

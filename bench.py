@@ -135,7 +135,7 @@ def gemm_bytes(work):
     return sum(4.0 * (4 * d * R + R * R) for (s, W, R, _) in work for d in s.shape)
 
 
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_v6_traffic.json")
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_v9_traffic.json")
 
 
 def load_traffic():

@@ -63,6 +63,8 @@ def load() -> ctypes.CDLL:
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
+        "admmq_set_solve_mode": (I32, [I32]),
+        "admmq_get_solve_mode": (I32, []),
         "admmq_debug_set_legacy_stage1": (I32, [I32]),
         "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
@@ -137,6 +139,28 @@ class exhaustive_search:
 
     def __exit__(self, *exc):
         load().admmq_set_exhaustive_search(0)
+        return False
+
+
+class solve_mode:
+    """Context manager: the per-iteration solve's operand form, ``"split"`` (default:
+    fp16 hi/lo planes on f16 MFMA) or ``"fp32"`` (fp32 MFMA). Restores the previous
+    mode on exit."""
+
+    MODES = {"fp32": 0, "split": 1}
+
+    def __init__(self, mode: str):
+        if mode not in self.MODES:
+            raise ValueError(mode)
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = load().admmq_get_solve_mode()
+        check(load().admmq_set_solve_mode(self.MODES[self.mode]), "set_solve_mode")
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_set_solve_mode(self.prev)
         return False
 
 

@@ -52,12 +52,27 @@ class LayerRun:
     loss: List[float] = field(default_factory=list)
     lossq: List[float] = field(default_factory=list)
     active: bool = True
+    # What the reference saves (scripts/factorize.py:315-318): the 3-way loop assigns
+    # `factors` after the loop (the latest sweep); the 2-way loop assigns it at the
+    # end of each sweep body, after the stop tests (:309-310), so a break leaves the
+    # previous sweep's factors (the initial ones before the first full sweep).
+    saved: List[torch.Tensor] = field(default_factory=list)
+    saved_quantized: List[Optional[torch.Tensor]] = field(default_factory=list)
 
     def __post_init__(self):
         if not self.duals:
             self.duals = [torch.zeros_like(f) for f in self.factors]
         if not self.quantized:
             self.quantized = [None] * len(self.factors)
+        if not self.saved:
+            self.saved = list(self.factors)
+            self.saved_quantized = list(self.quantized)
+
+    def result(self):
+        """(factors, quantized factors) as the reference's script would save them."""
+        if self.W.dim() == 3:
+            return list(self.factors), list(self.quantized)
+        return list(self.saved), list(self.saved_quantized)
 
 
 def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: int, qscheme: str,
@@ -65,17 +80,22 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
     """One ALS sweep over all active layers (modes batched across layers)."""
     act = [r for r in runs if r.active]
     nmodes = max((len(r.factors) for r in act), default=0)
+    infos = []
     for mode in range(nmodes):
         sel = [r for r in act if mode < len(r.factors)]
         GF = gram_mttkrp_batched([(r.W, r.factors) for r in sel], mode)
         probs = [(r.factors[mode], r.duals[mode], F, G) for r, (G, F) in zip(sel, GF)]
-        Hs = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
-                                    check_spd=False)
+        # no per-call sync for the SPD test: the flags are read once per sweep (below)
+        Hs, info = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
+                                          check_spd=False, return_info=True)
+        infos.append(info[:, 2])
         for r, H in zip(sel, Hs):
             r.factors[mode] = H
         qs = quantize_batched(Hs, bits, qscheme, num_attempts=num_attempts)
         for r, q in zip(sel, qs):
             r.quantized[mode] = q
+    if infos:
+        check_spd_flags(infos, act, nmodes)
     if not record_errors:
         return
     errs = rel_error_batched([(r.W, r.factors) for r in act] + [(r.W, r.quantized) for r in act])
@@ -87,6 +107,24 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
             r.active = False
         elif len(r.loss) > 10 and r.loss[-1] - r.loss[-back] > 1e-3:
             r.active = False
+        else:   # the 2-way script's end-of-body assignment (scripts/factorize.py:309-310)
+            r.saved, r.saved_quantized = list(r.factors), list(r.quantized)
+
+
+def check_spd_flags(infos, runs, nmodes):
+    """source/admm.py:54 raises torch.linalg.LinAlgError when G + rho I is not SPD.
+    The batched driver reads every mode's device flag in ONE host sync per sweep and
+    raises the same error, naming the first failing (layer, mode)."""
+    flags = torch.cat(infos).cpu()
+    if int(flags.max()) == 0:
+        return
+    k = int(torch.nonzero(flags)[0])
+    for mode in range(nmodes):
+        sel = [r for r in runs if mode < len(r.factors)]
+        if k < len(sel):
+            raise torch.linalg.LinAlgError(f"linalg.cholesky: The factorization could not be completed because the "
+                                           f"input is not positive-definite (layer {sel[k].name}, mode {mode}).")
+        k -= len(sel)
 
 
 def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_iter_als: int, max_iter_admm: int,
@@ -105,6 +143,7 @@ def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_
             e, eq = rel_error_batched([(W, fs), (W, q)])
             run.loss.append(e)
             run.lossq.append(eq)
+            run.saved_quantized = list(q)
         runs.append(run)
     for _ in range(max_iter_als):
         if not any(r.active for r in runs):
@@ -168,7 +207,7 @@ def main(argv=None):
     if args.method == 'admm':
         run = factorize_layers([weight], [args.rank], args.max_iter_als, args.max_iter_admm, args.bits, args.qscheme,
                                args.init, args.seed, names=[args.layer])[0]
-        factors, factors_q = run.factors, run.quantized
+        factors, factors_q = run.result()
         torch.save(run.loss, os.path.join(outdir, fileprefix + '_losshist.pt'))
         torch.save(run.lossq, os.path.join(outdir, fileprefix + '_lossquanthist.pt'))
     else:

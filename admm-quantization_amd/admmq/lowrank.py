@@ -74,11 +74,23 @@ class SubspaceProjector:
         return Ur @ torch.diag(S[:r]) @ Vt[:r]
 
 
+def _is_device_quantizer(f) -> bool:
+    return isinstance(f, partial) and f.func is quantize_tensor
+
+
 def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.Tensor,
                    proj_func: Callable[[torch.Tensor], torch.Tensor], rho: float = 1.0, max_iter: int = 50,
-                   eps: float = 1e-8, poll: int = 8, return_iters: bool = False):
+                   eps: float = 1e-8, poll: Optional[int] = None, return_iters: bool = False):
     """scripts/factorize_lowrank.py:85-101. Returns (H, U); U is updated in place and
-    returned (as in the reference); the caller's H is not written."""
+    returned (as in the reference); the caller's H is not written.
+
+    The break flag is read before an iteration's projection every ``poll``
+    iterations. Default: 8 for the HIP quantizer (queued without a host round trip;
+    an iteration queued after the break is a device no-op), 1 for any other
+    projection (an SVD synchronises anyway, and a projection of a stale iterate
+    after the break would cost a full SVD)."""
+    if poll is None:
+        poll = 8 if _is_device_quantizer(proj_func) else 1
     for t in (H, U, W, H2):
         _lib.require_device(t)
     if not (H.shape == U.shape == W.shape == H2.shape):
@@ -95,6 +107,8 @@ def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.
     wsp, wsn = _lib.ptr(ws), ws.numel()
     _lib.check(lib.admmq_lowrank_reset(wsp, wsn, s), "lowrank_reset")
     for j in range(1, max_iter):
+        if poll and j > 1 and (j - 1) % poll == 0 and int(ws[:4].view(torch.int32)[0]):
+            break
         _lib.check(lib.admmq_lowrank_pre(_lib.ptr(Hc), _lib.ptr(Uc), _lib.ptr(Wc), _lib.ptr(H2c), _lib.ptr(Hb),
                                          _lib.ptr(X), n, ctypes.c_float(rho), wsp, wsn, s), "lowrank_pre")
         Hn = proj_func(X).contiguous()
@@ -102,8 +116,6 @@ def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.
             raise ValueError("admmq.lowrank: proj_func must return a float32 tensor of X's shape on X's device")
         _lib.check(lib.admmq_lowrank_post(_lib.ptr(Hn), _lib.ptr(Hb), _lib.ptr(Hc), _lib.ptr(Uc), n,
                                           ctypes.c_float(eps), wsp, wsn, s), "lowrank_post")
-        if poll and j % poll == 0 and int(ws[:4].view(torch.int32)[0]):
-            break
     if Uc is not U:
         U.copy_(Uc)
     iters = int(ws[:12].view(torch.int32)[2])

@@ -65,15 +65,19 @@ __global__ __launch_bounds__(256) void k_fill_a64(const ProbDesc* __restrict__ p
   }
 }
 
+// Work unit = whole rows [start / ld, total / ld) of one problem (at most 1024 G
+// elements), so a split problem's next P gets its exact per-row exponent in one pass.
 template <int G>   // float4 groups per thread: 256 G * 4 elements per work unit
 __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restrict__ probs, const Chunk* __restrict__ chunks,
                                                        int ncand, int bits, int scheme, int slot, int iter) {
+  constexpr int kMaxRows = 1024 * G / 32;   // ld >= 32
+  __shared__ unsigned rmax[kMaxRows];
   const Chunk ck = chunks[blockIdx.x];
   // float4 group g of thread t at start + 4 t + 1024 g. The stop flag, then the element
   // loads, straight from the unit (no descriptor read first; past the end a clamped
   // address, never used): independent of the quantizer parameters, so their latency
   // overlaps the parameter chain (descriptor -> stat -> sel -> sse) below.
-  const long long total = ck.total;
+  const long long total = ck.total;   // end of this unit
   const int stopped = gld_i32(ck.done);
   float4 t4[G], h4[G], u4[G], f4[G];
 #pragma unroll
@@ -87,12 +91,20 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
   }
   const ProbDesc& p = probs[ck.job];
   if (stopped) return;   // converged earlier (sticky break)
-  const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);
+  if (p.split) {
+    for (int r = threadIdx.x; r < kMaxRows; r += 256) rmax[r] = 0u;
+    __syncthreads();
+  }
+  const QParams qp = block_qparams(scheme, bits, p.mv, slot, ncand, 0, 0.f, 0.f);   // (ends with a barrier)
   const float rho = p.rho[0];
+  const bool split = p.split != 0;
+  const int row0 = ck.start / p.ld;
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  float4 p4[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
+    p4[g] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e >= total) continue;
     const int row = (int)(e / p.ld);
     const int c0 = (int)(e - (long long)row * p.ld);
@@ -118,7 +130,26 @@ __global__ __launch_bounds__(256) void k_finalize_admm(const ProbDesc* __restric
     }
     *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
     *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
-    *reinterpret_cast<float4*>(p.P + e) = make_float4(po[0], po[1], po[2], po[3]);
+    p4[g] = make_float4(po[0], po[1], po[2], po[3]);
+    if (!split) {
+      *reinterpret_cast<float4*>(p.P + e) = p4[g];
+    } else {   // a float4 never straddles a row (ld % 32 == 0)
+      const float m = fmaxf(fmaxf(fabsf(po[0]), fabsf(po[1])), fmaxf(fabsf(po[2]), fabsf(po[3])));
+      atomicMax(&rmax[row - row0], __float_as_uint(m));
+    }
+  }
+  if (split) {
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * g;
+      if (e >= total) continue;
+      const int row = (int)(e / p.ld);
+      const int c0 = (int)(e - (long long)row * p.ld);
+      const int ex = split_exponent(__uint_as_float(rmax[row - row0]));
+      split_store4(p.P2 + (size_t)row * 2 * p.ld, c0, p4[g], ex);
+      if (c0 == 0) p.eP[row] = ex;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -169,13 +200,18 @@ void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s) {
   const int nb = (int)std::min<long long>(1024, (tot + 255) / 256);
   hipLaunchKernelGGL(k_fill_a64, dim3(nb, nprob), dim3(256), 0, s, d);
 }
-void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int chunk_elems, int ncand, int bits,
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int groups, int ncand, int bits,
                           int qscheme, int slot, int iter, hipStream_t s) {
   if (nchunks <= 0) return;
-  if (chunk_elems == 4096)
-    hipLaunchKernelGGL(k_finalize_admm<4>, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
-  else
-    hipLaunchKernelGGL(k_finalize_admm<1>, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter);
+#define ADMMQ_FIN(G) \
+  hipLaunchKernelGGL(k_finalize_admm<G>, dim3(nchunks), dim3(256), 0, s, d, chunks, ncand, bits, qscheme, slot, iter)
+  switch (groups) {
+    case 1: ADMMQ_FIN(1); break;
+    case 2: ADMMQ_FIN(2); break;
+    case 4: ADMMQ_FIN(4); break;
+    default: ADMMQ_FIN(8); break;
+  }
+#undef ADMMQ_FIN
 }
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s) {
   const long long tot = (long long)maxI * maxR;

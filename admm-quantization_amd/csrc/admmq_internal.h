@@ -2,7 +2,7 @@
 //
 // Memory layout in HBM (per ADMM problem = one (layer, mode) factor):
 //   Fp, H, U, P, X, HT : float32 [Ip x ld] row-major, ld = roundup(R,32),
-//                        Ip = 32 if I <= 32 else roundup(I, 32 WM) (WM = big GEMM tile rows / 32);
+//                        Ip = 32 if I <= 32 else roundup(I, 64);
 //                        pads kept at exactly 0
 //   M                  : float32 [ldm x ldm], ldm = roundup(R,64); (G+rho I)^-1,
 //                        symmetric, zero outside the R x R block
@@ -16,9 +16,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic per-block timelines / counters (admmq_debug_*_trace, tools/*_timeline.py):
+// compiled in only with `make TRACE=1`; the production library makes no trace stores.
+#ifndef ADMMQ_TRACE
+#define ADMMQ_TRACE 0
+#endif
+#define ADMMQ_NOW() (ADMMQ_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull)
+
 namespace admmq {
 
 enum QScheme { kMse = 0, kMinMax = 1, kSymmetric = 2, kAffine = 3 };
+enum SolveMode { kSolveF32 = 0, kSolveSplit = 1 };
 
 constexpr int kMaxSel = 64;        // stage-2 candidate list length (else exhaustive)
 constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage search
@@ -65,6 +73,10 @@ struct ProbDesc {
   float* Fp; float* H; float* U; float* P; float* X; float* HT;
   float* M;
   double* A64; double* L64; double* D64;   // D64: diagonal L blocks [nbk][32][32]
+  // split solve (kSolveSplit, gemm_kernels.hip): P and M as [rows][ld/32][32 hi | 32 lo]
+  // fp16 planes (the bytes of the fp32 rows) with one power-of-two exponent per row
+  _Float16* P2; int* eP;    // [Ip] rows
+  _Float16* M2; int* eM;    // [ldm] rows
   MseView mv;
   double* res;
   float* Part;     // thin factors (I <= kThinRows): split-K partial sums [nkg][NR][ld]
@@ -73,6 +85,8 @@ struct ProbDesc {
   float* rho;
   int I, R, ld, Ip, ldm, nbk;
   int nq;          // quads of the valid (I x R) region: I * ceil(R/4)
+  int split;       // 1: this problem's solve uses the split operand planes
+  int fin_rows;    // split: rows per finalize unit (units hold whole rows)
   int pad_;
 };
 
@@ -88,13 +102,14 @@ struct QJob {
 };
 
 // Work-unit tables (built on the host, uploaded once per call)
-// GEMM tile: rows tm, columns tn of problem prob, K-steps [k0, k0 + nk). part >= 0: one
-// half (ks = 0 / 1) of a split-K pair, whose second-arriving half finishes the tile.
-// The operands' addresses and strides ride along (filled at upload), so a tile's first
-// loads depend on the tile entry only, not on a further descriptor read.
+// GEMM tile: rows tm, columns tn of problem prob, K-steps nk. The operands' addresses
+// and strides ride along (filled at upload), so a tile's first loads depend on the
+// tile entry only, not on a further descriptor read. Split form: P / M point at the
+// fp16 planes (row strides in floats are unchanged), eP / eM at the row exponents.
 struct GemmTile {
-  int prob, tm, tn, first, k0, nk, part, ks;
+  int prob, tm, tn, first, nk, pad_;
   const float* P; const float* M; const float* U;
+  const int* eP; const int* eM;
   int ld, ldm;
 };
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
@@ -160,18 +175,14 @@ void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
                       int ncand, hipStream_t s);
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
-                 float* kpart, unsigned* pcnt, int slot, int iter, float eps, int ncand, hipStream_t s);
-int gemm_split_min_steps();
-int gemm_persistent_per_cu();
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
+                 int iter, float eps, int ncand, hipStream_t s);
+void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);
 size_t hist_lds_bytes(int ncand, int bits);
 size_t hist3_lds_bytes(int ncand, int bits);
-int copy_thin_trace(unsigned long long* host, int n);
-int copy_gemm_trace(unsigned long long* host, int n);
-int gemm_big_wm();
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);
@@ -187,7 +198,7 @@ void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ng
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s);
 void launch_mse_sse(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                     int slot, hipStream_t s);
-void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int chunk_elems, int ncand, int bits,
+void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, int groups, int ncand, int bits,
                           int qscheme, int slot, int iter, hipStream_t s);
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
 

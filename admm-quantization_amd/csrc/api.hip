@@ -1,6 +1,7 @@
 // C-ABI of libadmmq: workspace planning and stream-ordered launch sequences.
 // See include/admmq.h for the contract and the reference interfaces replaced.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -55,19 +56,13 @@ struct Prof {
   bool sampled = true;  // the current iteration is timed
 };
 static Prof g_prof;
-// A/B switch: evaluate all candidates exhaustively instead of the two-stage search.
-static bool g_exhaustive = false;
-// Small jobs (I <= kThinRows) run stage 1, selection, stage 2 and finalize in one block
-// each (ADMMQ_SMALL_FUSED=0: the multi-block stage 1 + finalize launches instead).
-static bool g_small_fused = !getenv("ADMMQ_SMALL_FUSED") || atoi(getenv("ADMMQ_SMALL_FUSED")) != 0;
-// Big GEMM tiles dealt to CUs by K-steps (ADMMQ_GEMM_CUBAL=0: longest-first order only).
-static bool g_cu_balance = !getenv("ADMMQ_GEMM_CUBAL") || atoi(getenv("ADMMQ_GEMM_CUBAL")) != 0;
-// Big GEMM tiles placed by whole layers per XCD (ADMMQ_GEMM_XCD=1; default: the column-interleaved order).
-static bool g_xcd_layers = getenv("ADMMQ_GEMM_XCD") && atoi(getenv("ADMMQ_GEMM_XCD")) != 0;
-// Stage-1 form: merged thresholds (k_mse_hist3, default where supported) or per-level
-// (k_mse_hist; ADMMQ_STAGE1=legacy, and wherever merged_tables/merged_ok decline). Both
-// give the same integers.
-static bool g_legacy_stage1 = getenv("ADMMQ_STAGE1") && std::string(getenv("ADMMQ_STAGE1")) == "legacy";
+// Process-wide switches (atomics: set from any thread, read by the launch sequences).
+// exhaustive: evaluate all candidates (reference-style) instead of the two-stage search;
+// legacy stage 1: the per-level stage-1 form instead of merged thresholds (same integers);
+// solve mode: kSolveSplit (default) or kSolveF32 for the per-iteration GEMM.
+static std::atomic<bool> g_exhaustive{false};
+static std::atomic<bool> g_legacy_stage1{false};
+static std::atomic<int> g_solve_mode{kSolveSplit};
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
@@ -145,10 +140,7 @@ struct AdmmPlan {
   Chunk* d_sse = nullptr;
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
-  unsigned* d_queue = nullptr;   // GEMM ticket counters {big, small}
-  int nsplit = 0;                // split-K tile pairs
-  float* d_kpart = nullptr;      // [nsplit][2][(32 WM) x 64] partial sums (big tiles)
-  unsigned* d_pcnt = nullptr;    // [nsplit] arrival counters (zeroed per run)
+  bool split = false;            // per-iteration solve on the split fp16 planes (kSolveSplit)
   std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
   ThinUnit* d_thin = nullptr;
   unsigned* d_tcnt = nullptr;    // their per-column-block arrival counters
@@ -158,7 +150,7 @@ struct AdmmPlan {
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
   int ntiles_big = 0, ntiles_small = 0;
-  int fin_elems = kElemChunk;
+  int fin_groups = 1;             // float4 groups per thread of the finalize units
   int hist_nv = 1;
   std::vector<int> small;         // jobs with I <= kThinRows (one-block fused search + finalize)
   int* d_small = nullptr;
@@ -166,17 +158,10 @@ struct AdmmPlan {
   int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
 };
 
-// Thin factors (I <= kThinRows) take the VALU split-K solve (k_gemm_thin) unless
-// ADMMQ_GEMM_THIN=0 (A/B: the 32 x 64 MFMA tiles instead).
-static bool thin_enabled() {
-  static const bool on = !(getenv("ADMMQ_GEMM_THIN") && std::string(getenv("ADMMQ_GEMM_THIN")) == "0");
-  return on;
-}
-
 static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
   GemmTile t;
-  t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.k0 = 0; t.nk = nk; t.part = -1; t.ks = 0;
-  t.P = nullptr; t.M = nullptr; t.U = nullptr; t.ld = 0; t.ldm = 0;   // set at upload
+  t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.nk = nk; t.pad_ = 0;
+  t.P = nullptr; t.M = nullptr; t.U = nullptr; t.eP = nullptr; t.eM = nullptr; t.ld = 0; t.ldm = 0;   // set at upload
   return t;
 }
 
@@ -208,69 +193,18 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
     for (int r = 0; r < (int)bins[b].size(); ++r) tiles[b + (size_t)r * ncu] = bins[b][r];
 }
 
-// Whole-layer XCD placement of the big GEMM tiles. Workgroup b runs on XCD b % 8
-// (round-robin dispatch; every tile of a launch is resident at once), and an XCD's
-// L2 serves its workgroups only: a layer whose tiles are spread over all 8 XCDs is
-// fetched from the Infinity Cache 8 times (P once per XCD, M once per column slab),
-// one kept on one XCD about once. Layers are cut into column-tile ranges of at most
-// an eighth of the launch's MFMA work and placed largest first on the least-loaded
-// XCD (LPT); each XCD's list runs longest K first, tm-major within a column group.
-// Position p of the table takes the next tile of XCD p % 8 (another XCD's when that
-// list has run out).
-static void order_tiles_by_xcd(AdmmPlan& pl, const std::vector<int>& order) {
-  struct Piece { int prob, tn0, tn1; double work; };
-  std::vector<Piece> pieces;
-  double total = 0.0;
-  const int bm = 32 * gemm_big_wm();
-  for (int i : order) {
-    const ProbDesc& d = pl.desc[i];
-    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip == 32) continue;
-    total += (double)(d.Ip / bm) * ((d.ld + 63) / 64) * d.ld;
+// Finalize units hold whole rows (the split solve needs each row's exponent in one pass):
+// at most 1024 G elements, G in {1, 2, 4, 8}. Returns G.
+static int fin_groups_for(const std::vector<ProbDesc>& desc, const std::vector<int>& jobs) {
+  long long units4k = 0;
+  int maxld = 0;
+  for (int i : jobs) {
+    units4k += ((long long)desc[i].I * desc[i].ld + kFinElems - 1) / kFinElems;
+    maxld = std::max(maxld, desc[i].ld);
   }
-  const double cap = total / 8.0;
-  for (int i : order) {
-    const ProbDesc& d = pl.desc[i];
-    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip == 32) continue;
-    const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
-    const double col_work = (double)TM * d.ld;
-    const int npieces = std::max(1, (int)std::ceil(col_work * TN / cap - 1e-9));
-    for (int q = 0; q < npieces; ++q) {
-      const int a = TN * q / npieces, b = TN * (q + 1) / npieces;
-      if (b > a) pieces.push_back({i, a, b, col_work * (b - a)});
-    }
-  }
-  std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& x, const Piece& y) { return x.work > y.work; });
-  std::vector<std::vector<GemmTile>> lists(8);
-  double load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  std::vector<std::vector<Piece>> own(8);
-  for (const Piece& pc : pieces) {
-    const int x = (int)(std::min_element(load, load + 8) - load);
-    load[x] += pc.work;
-    own[x].push_back(pc);
-  }
-  for (int x = 0; x < 8; ++x) {
-    std::stable_sort(own[x].begin(), own[x].end(),
-                     [&](const Piece& a, const Piece& b) { return pl.desc[a.prob].ld > pl.desc[b.prob].ld; });
-    for (const Piece& pc : own[x]) {
-      const ProbDesc& d = pl.desc[pc.prob];
-      const int TM = d.Ip / bm;
-      for (int g0 = pc.tn0; g0 < pc.tn1; g0 += 8)
-        for (int tm = 0; tm < TM; ++tm)
-          for (int tn = g0; tn < std::min(pc.tn1, g0 + 8); ++tn)
-            lists[x].push_back(mk_tile(pc.prob, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
-    }
-  }
-  size_t n = 0, pos[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (auto& l : lists) n += l.size();
-  for (size_t p = 0; p < n; ++p) {
-    int x = (int)(p % 8);
-    if (pos[x] >= lists[x].size()) {   // this XCD's list is done: take from the longest remaining one
-      size_t best = 0;
-      for (int y = 0; y < 8; ++y)
-        if (lists[y].size() - pos[y] > best) { best = lists[y].size() - pos[y]; x = y; }
-    }
-    pl.tiles.push_back(lists[x][pos[x]++]);
-  }
+  int g = units4k >= kFinMinUnits ? 4 : 1;   // small problem sets keep their parallelism
+  while (g < 8 && 1024 * g < maxld) g *= 2;
+  return g;
 }
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
@@ -280,7 +214,10 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.desc.resize(nprob);
   pl.thin_nr = 0;
   for (int i = 0; i < nprob; ++i)
-    if (thin_enabled() && probs[i].I > 0 && probs[i].I <= kThinRows) pl.thin_nr = std::max(pl.thin_nr, probs[i].I);
+    if (probs[i].I > 0 && probs[i].I <= kThinRows) pl.thin_nr = std::max(pl.thin_nr, probs[i].I);
+  pl.split = g_solve_mode.load() == kSolveSplit;
+  for (int i = 0; i < nprob; ++i)   // the split finalize needs whole rows in one unit
+    if (probs[i].I > kThinRows && rup(std::max(probs[i].R, 1), 32) > 8192) pl.split = false;
   for (int i = 0; i < nprob; ++i) {
     const admmq_problem& a = probs[i];
     if (a.I <= 0 || a.R <= 0) return fail(ADMMQ_ERR_ARG, "I and R must be positive");
@@ -291,10 +228,12 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, 32 * gemm_big_wm());
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, 64);
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
+    const bool thin = a.I <= kThinRows;
+    d.split = (pl.split && !thin) ? 1 : 0;
     const size_t fe = (size_t)d.Ip * d.ld;
     d.Fp = cv.take<float>(fe); d.H = cv.take<float>(fe); d.U = cv.take<float>(fe);
     d.P = cv.take<float>(fe); d.X = cv.take<float>(fe); d.HT = cv.take<float>(fe);
@@ -302,8 +241,13 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.A64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.L64 = cv.take<double>((size_t)d.ldm * d.ldm);
     d.D64 = cv.take<double>((size_t)d.ldm * 32);
+    if (d.split) {
+      d.P2 = cv.take<_Float16>(2 * fe);
+      d.eP = cv.take<int>(d.Ip);
+      d.M2 = cv.take<_Float16>(2 * (size_t)d.ldm * d.ldm);
+      d.eM = cv.take<int>(d.ldm);
+    }
     d.res = cv.take<double>(2 * kResRep * 4);
-    const bool thin = pl.thin_nr > 0 && a.I <= kThinRows;
     d.Part = thin ? cv.take<float>((size_t)((d.ld + kThinK - 1) / kThinK) * pl.thin_nr * d.ld) : nullptr;
     d.tcnt = nullptr;
     d.flags = cv.take<int>(4);
@@ -316,56 +260,28 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
   }
   // GEMM tiles, longest K first (LPT over the grid); `first` marks tile (0,0).
-  // (32 WM)x64 tiles (Ip > 32) first, then the 32x64 tiles of the thin (I <= 32) factors.
+  // 64x64 tiles (Ip > 32) first, then the 32x64 tiles of the 17..32-row factors.
+  // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
+  // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
+  // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
   pl.tiles.clear();
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip == 32) continue;   // thin: k_gemm_thin units below; 32-row tiles after
+    const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
+    for (int g0 = 0; g0 < TN; g0 += 8)
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
+          pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+  }
+  order_tiles_for_cus(pl.tiles, 256, 3);
   std::vector<GemmTile> small;
-  if (g_xcd_layers) {
-    order_tiles_by_xcd(pl, order);
-  } else {
-    // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
-    // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
-    // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
-    for (int i : order) {
-      const ProbDesc& d = pl.desc[i];
-      const int bm = d.Ip == 32 ? 32 : 32 * gemm_big_wm();
-      if (pl.thin_nr > 0 && d.I <= kThinRows) continue;   // thin: k_gemm_thin units below
-      if (d.Ip == 32) continue;
-      const int TM = d.Ip / bm, TN = (d.ld + 63) / 64;
-      for (int g0 = 0; g0 < TN; g0 += 8)
-        for (int tm = 0; tm < TM; ++tm)
-          for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
-            pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
-    }
-  }
-  // Split-K: a big tile of >= gemm_split_min_steps() K-steps becomes two halves (one
-  // workgroup each; partial pair `part`), so the grid's work units are of similar
-  // length and the hardware's dispatch of the tail balances the CUs; units then run
-  // longest first (stable: the XCD-aware order within equal lengths).
-  pl.nsplit = 0;
-  if (gemm_split_min_steps() > 0) {
-    std::vector<GemmTile> out;
-    out.reserve(pl.tiles.size() * 2);
-    std::vector<GemmTile> second;
-    for (const GemmTile& t : pl.tiles) {
-      if (t.nk < gemm_split_min_steps()) { out.push_back(t); continue; }
-      GemmTile a = t, b = t;
-      a.nk = t.nk / 2; a.part = pl.nsplit; a.ks = 0;
-      b.k0 = a.nk; b.nk = t.nk - a.nk; b.part = pl.nsplit; b.ks = 1; b.first = 0;
-      ++pl.nsplit;
-      out.push_back(a);
-      second.push_back(b);
-    }
-    out.insert(out.end(), second.begin(), second.end());
-    std::stable_sort(out.begin(), out.end(), [](const GemmTile& x, const GemmTile& y) { return x.nk > y.nk; });
-    pl.tiles.swap(out);
-  }
-  if (g_cu_balance && pl.nsplit == 0 && gemm_persistent_per_cu() == 0) order_tiles_for_cus(pl.tiles, 256, 3);
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
-    if ((pl.thin_nr > 0 && d.I <= kThinRows) || d.Ip != 32) continue;
+    if (d.I <= kThinRows || d.Ip != 32) continue;
     const int TN = (d.ld + 63) / 64;
     for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
   }
@@ -378,7 +294,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<int> tcnt_off(nprob, -1);
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
-    if (!(pl.thin_nr > 0 && d.I <= kThinRows)) continue;
+    if (d.I > kThinRows) continue;
     const int nkg = (d.ld + kThinK - 1) / kThinK, ncb = (d.ld + kThinCols - 1) / kThinCols;
     tcnt_off[i] = pl.ntcnt;
     pl.ntcnt += ncb;
@@ -388,28 +304,33 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
   pl.hist_chunks.clear();
-  long long big_units = 0, hist_units = 0;
+  long long hist_units = 0;
+  std::vector<int> big_jobs;
   for (int i = 0; i < nprob; ++i) {
-    big_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kFinElems - 1) / kFinElems;
     hist_units += ((long long)pl.desc[i].I * pl.desc[i].ld + kHistElems - 1) / kHistElems;
+    if (pl.desc[i].I > kThinRows) big_jobs.push_back(i);
   }
-  pl.fin_elems = big_units >= kFinMinUnits ? kFinElems : kElemChunk;
+  pl.fin_groups = fin_groups_for(pl.desc, big_jobs.empty() ? order : big_jobs);
   pl.hist_nv = hist_units > kHistMaxUnits ? 2 : 1;   // one round of resident stage-1 blocks
   // stage-1 / finalize units of the small jobs (I <= kThinRows) go last: when their
   // fused one-block path runs (k_mse_small_admm), the launches take only the others
   pl.small.clear();
+  const long long fin_cap = 1024LL * pl.fin_groups;
   for (int pass = 0; pass < 2; ++pass) {
     for (int i : order) {
-      const ProbDesc& d = pl.desc[i];
+      ProbDesc& d = pl.desc[i];
       if ((d.I <= kThinRows) != (pass == 1)) continue;
       if (pass == 1) pl.small.push_back(i);
       for (int q = 0; q < d.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
       const long long tot = (long long)d.I * d.ld;
-      for (long long e = 0; e < tot; e += pl.fin_elems)
-        pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot, d.H, d.Fp});
+      // whole rows per unit (rows longer than a unit: plain chunks; never a split problem)
+      const long long step = d.ld <= fin_cap ? (fin_cap / d.ld) * d.ld : fin_cap;
+      d.fin_rows = d.ld <= fin_cap ? (int)(fin_cap / d.ld) : 0;
+      for (long long e = 0; e < tot; e += step)
+        pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + step), d.H, d.Fp});
       const long long hu = (long long)kHistElems * pl.hist_nv;
       for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
-      pl.desc[i].mv.nhist = (int)((tot + hu - 1) / hu);
+      d.mv.nhist = (int)((tot + hu - 1) / hu);
     }
     if (pass == 0) { pl.nfin_big = (int)pl.fin_chunks.size(); pl.nhist_big = (int)pl.hist_chunks.size(); }
   }
@@ -422,9 +343,6 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
-  pl.d_queue = cv.take<unsigned>(2);
-  pl.d_kpart = cv.take<float>((size_t)std::max(pl.nsplit, 1) * 2 * (32 * gemm_big_wm()) * 64);
-  pl.d_pcnt = cv.take<unsigned>(std::max(pl.nsplit, 1));
   pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
   pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
   for (int i = 0; i < nprob; ++i)
@@ -440,7 +358,13 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_desc, pl.desc.data(), pl.desc.size() * sizeof(ProbDesc), s))) return rc;
   for (GemmTile& t : pl.tiles) {
     const ProbDesc& d = pl.desc[t.prob];
-    t.P = d.P; t.M = d.M; t.U = d.U; t.ld = d.ld; t.ldm = d.ldm;
+    t.U = d.U; t.ld = d.ld; t.ldm = d.ldm;
+    if (d.split) {   // the fp16 planes keep the fp32 rows' strides (in floats)
+      t.P = reinterpret_cast<const float*>(d.P2); t.M = reinterpret_cast<const float*>(d.M2);
+      t.eP = d.eP; t.eM = d.eM;
+    } else {
+      t.P = d.P; t.M = d.M;
+    }
   }
   if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
@@ -578,6 +502,14 @@ int32_t admmq_set_exhaustive_search(int32_t enable) {
   return ADMMQ_OK;
 }
 
+int32_t admmq_set_solve_mode(int32_t mode) {
+  if (mode != kSolveF32 && mode != kSolveSplit) return fail(ADMMQ_ERR_ARG, "solve mode must be 0 (fp32) or 1 (split)");
+  g_solve_mode = mode;
+  return ADMMQ_OK;
+}
+
+int32_t admmq_get_solve_mode(void) { return g_solve_mode.load(); }
+
 // diagnostics (not in include/admmq.h): workspace bytes of the plan carved against a
 // non-null base (no memory is touched), so a test can check that sizing (null base)
 // and the real carve agree
@@ -648,6 +580,10 @@ int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t nu
   launch_pack(pl.d_desc, nprob, pl.maxIp, pl.maxld, s);
   launch_fill_a64(pl.d_desc, nprob, pl.maxldm, s);
   launch_spd_inverse(pl.d_desc, nprob, pl.maxnbk, s);
+  if (pl.split) {   // fp16 planes of M and of the first right-hand side P
+    launch_split_rows(pl.d_desc, nprob, pl.maxldm, 1, s);
+    launch_split_rows(pl.d_desc, nprob, pl.maxIp, 0, s);
+  }
   prof_mark(s);
   return check_hip("admm_prepare");
 }
@@ -664,9 +600,6 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   hipStream_t s = static_cast<hipStream_t>(stream);
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
-  if (hipMemsetAsync(pl.d_queue, 0, 2 * sizeof(unsigned), s) != hipSuccess) return check_hip("queue reset");
-  if (pl.nsplit && hipMemsetAsync(pl.d_pcnt, 0, pl.nsplit * sizeof(unsigned), s) != hipSuccess)
-    return check_hip("split counter reset");
   if (pl.ntcnt && hipMemsetAsync(pl.d_tcnt, 0, pl.ntcnt * sizeof(unsigned), s) != hipSuccess)
     return check_hip("thin counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
@@ -680,14 +613,13 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
     if (ngroups && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
   }
-  const bool fuse_small = g_small_fused && qscheme == kMse && !exhaustive && merged && !pl.small.empty() &&
+  const bool fuse_small = qscheme == kMse && !exhaustive && merged && !pl.small.empty() &&
                           pl.small_groups > 0 && num_attempts <= 1024;
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     prof_class(0); prof_mark(s);
-    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.d_queue, pl.d_kpart, pl.d_pcnt, slot, it,
-                eps, num_attempts, s);
+    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps, num_attempts, s);
     launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
     prof_mark(s);
     if (qscheme == kMse) {
@@ -708,7 +640,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
       prof_mark(s);
     }
     prof_class(2); prof_mark(s);
-    launch_finalize_admm(pl.d_desc, pl.d_fin, fuse_small ? pl.nfin_big : nfin, pl.fin_elems, num_attempts, bits,
+    launch_finalize_admm(pl.d_desc, pl.d_fin, fuse_small ? pl.nfin_big : nfin, pl.fin_groups, num_attempts, bits,
                          qscheme, slot, it, s);
     prof_mark(s);
   }
@@ -718,9 +650,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   return check_hip("admm_run");
 }
 
-// diagnostics (not in include/admmq.h): per-workgroup timeline of the last GEMM launch
-int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
-int32_t admmq_debug_thin_trace(unsigned long long* host, int32_t n) { return copy_thin_trace(host, n); }
+// diagnostics (not in include/admmq.h): per-block timelines of the last launches (make TRACE=1)
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }
@@ -750,7 +680,7 @@ int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, 
   int rc = plan_quant(t, n, num_attempts, workspace, pl);
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
-  return run_quant(pl, n, bits, qscheme, num_attempts, static_cast<hipStream_t>(stream), true, g_exhaustive);
+  return run_quant(pl, n, bits, qscheme, num_attempts, static_cast<hipStream_t>(stream), true, g_exhaustive.load());
 }
 
 int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,

@@ -1,38 +1,47 @@
 // ADMM primal solve (source/admm.py:56-57):  H_T = (F + rho(H+U)) (G + rho I)^-1
-// as one grouped fp32-MFMA GEMM  HT[Ip x ld] = P[Ip x ld] . M[ld x ld]  over every
-// active (layer, mode) problem. P is produced by the previous iteration's
-// finalize kernel; M is symmetric, so the B operand is read as rows of M.
+// as one grouped MFMA GEMM  HT[Ip x ld] = P[Ip x ld] . M[ld x ld]  over every active
+// (layer, mode) problem. P is produced by the previous iteration's finalize kernel; M is
+// symmetric, so the B operand is read as rows of M.
+//
+// Two operand forms (admmq_set_solve_mode):
+//   kSolveF32    P and M in fp32, v_mfma_f32_32x32x2_f32 (an fp32 FMA chain).
+//   kSolveSplit  P and M each stored as two fp16 planes per row, scaled by a power of
+//                two per row: x 2^e = hi + lo with hi = fp16(x 2^e), lo = fp16(x 2^e - hi)
+//                (|x - (hi + lo) 2^-e| <= 2^-22 |x|). Then
+//                    H_T = 2^-(eP_i + eM_j) (Ph Mh + Ph Ml + Pl Mh)
+//                on v_mfma_f32_32x32x16_f16 (16x the fp32 MFMA rate, 3 products, fp32
+//                accumulation): per product about 2^-21 relative, the size of the fp32
+//                GEMM's own accumulation error at K ~ 1000. The planes take the bytes of
+//                the fp32 operand, so the kernel moves the same data at 5x less MFMA time.
 //
 // Tile (32*WM) x 64 per workgroup of 2*WM*KS waves; the KS waves (ks, wm, wn) own the
-// 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
-// chain over its 1/KS slice of every K-step, summed in fixed order through LDS at the
-// end. WM = 2 (64 x 64 tiles) for factors with I > 32, WM = 1 (32 x 64) for the 9-row
-// mode-C factors.
+// 32 x 32 sub-tile at (32 wm, 32 wn), each with one accumulator chain over its 1/KS slice
+// of every K-step, summed in fixed order through LDS at the end. WM = 2 (64 x 64 tiles)
+// for factors with I > 32, WM = 1 (32 x 64) for 17..32-row factors.
 //
-// Staging: K-step 32 (128 B per operand row). Both operands go global -> LDS by
-// global_load_lds_dwordx4 (no VGPR round trip) into an NS-deep ring of stages, NS-1
-// K-steps in flight; each wave waits with a counted vmcnt for its own pieces of the
-// stage it is about to read and a raw s_barrier publishes the stage (a __syncthreads
-// would drain every in-flight load). A stage image is row-major, 128 B per row, with
-// the 16-B chunk c of row r stored at chunk position c ^ ((r >> 1) & 7) - applied on
-// the global source address, since an LDS-DMA writes lane-linear - so the fragment
-// reads (ds_read_b128) are bank-conflict free for the gfx950 b128 lane groups.
-// The k-order inside a K-step is k = 16 h + m (lane half h, MFMA m): a lane's 16
-// operands are 64 contiguous bytes; A and B use the same order, so the product is
-// exact in any order and only the f32 rounding sequence differs.
+// Staging: K-step 32 (128 B per operand row in both forms: 32 floats, or 32 hi + 32 lo
+// halfs). Both operands go global -> LDS by global_load_lds_dwordx4 (no VGPR round trip)
+// into an NS-deep ring of stages, NS-1 K-steps in flight; each wave waits with a counted
+// vmcnt for its own pieces of the stage it is about to read and a raw s_barrier publishes
+// the stage (a __syncthreads would drain every in-flight load). A stage image is
+// row-major, 128 B per row, with the 16-B chunk c of row r stored at chunk position
+// c ^ ((r >> 1) & 7) - applied on the global source address, since an LDS-DMA writes
+// lane-linear - so the fragment reads (ds_read_b128) are bank-conflict free.
+// fp32: the k-order inside a K-step is k = 16 h + m (lane half h, MFMA m); split: chunk
+// 2 kc + h holds hi halfs k = 16 kc + 8 h .. +7 (the f16 MFMA's lane-half k group), chunk
+// 4 + 2 kc + h the matching lo halfs. A and B use the same order in either form.
 //
-// Epilogue: store HT, X = HT - U, and fold max|X|, min X, max X of the valid
-// region into the problem's per-iteration stat slot (one atomic each per block).
+// Epilogue: store HT (split: scaled back by ldexp), and fold max|X|, min X, max X of
+// X = HT - U over the valid region into the problem's per-iteration stat slot.
 #include <algorithm>
 #include <cstdlib>
-#include <type_traits>
-#include <utility>
 
 #include "quant_device.h"
 
 namespace admmq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BN = 64, BK = 32;
 
@@ -67,11 +76,6 @@ __device__ __forceinline__ float4 ldg4(const float* q) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// Per-tile timeline of the last GEMM launch (diagnostics: admmq_debug_gemm_trace):
-// {start, end} s_memrealtime ticks (100 MHz) and {workgroup, xcc, hw_id}.
-constexpr int kTraceMax = 8192;
-__device__ unsigned long long g_gemm_trace[kTraceMax][3];
-
 // Workgroup barrier that is also a compiler barrier for memory operations (the builtin
 // s_barrier is not: LDS reads of the next stage could be hoisted above it) and adds
 // no waitcnt of its own (unlike __syncthreads, which would drain in-flight glds).
@@ -84,23 +88,13 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// Grouped GEMM over a tile queue. gridDim.x workgroups take tiles in LPT order
-// (longest K first, as listed in `tiles`): the first tile of a workgroup is its
-// blockIdx, later ones come from a device-scope ticket counter drawn when the
-// workgroup's K-loop ends. Every launch draws exactly ntiles tickets (each workgroup's
-// last draw fails), so launch number `iter` of a run owns tickets
-// [iter * ntiles, (iter + 1) * ntiles) and the counter is zeroed once per run. With
-// gridDim.x == ntiles (the default) every workgroup runs exactly one tile and draws no ticket.
-//
-// Workgroup tile (32 WM) x 64 with 2 WM KS waves: the KS waves (ks, wm, wn) own the
-// 32 x 32 sub-tile at (32 wm, 32 wn), each with one v_mfma_f32_32x32x2_f32 accumulator
-// chain over its 1/KS slice of the k range of every K-step; the partials are summed in
-// fixed order at the end.
-template <int WM, int KS, int NS, int NA = 1>   // NA: independent accumulator chains per wave (1 or 2)
-__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? 3 : 1))) void k_gemm(const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles,
-                                                        int ntiles, unsigned* __restrict__ queue,
-                                                        float* __restrict__ kpart, unsigned* __restrict__ pcnt, int slot,
-                                                        int iter, float eps, int ncand) {
+__device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// One workgroup per tile (the grid is the tile list, longest K first, CU-balanced by the
+// planner). SPLIT selects the operand form (see the file header).
+template <int WM, int KS, int NS, bool SPLIT>
+__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? 3 : 1))) void k_gemm(
+    const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
   constexpr int NSUB = 2 * WM;                 // 32 x 32 sub-tiles per workgroup
   constexpr int NW = NSUB * KS;                // waves
@@ -109,11 +103,12 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   constexpr int STAGE = ROWS * 32;             // floats per stage
   constexpr int NG = ROWS / 8;                 // glds wave-instructions per stage (8 rows each)
   constexpr int GPW = NG / NW;                 // ... per wave
-  constexpr int QS = 4 / KS;                   // b128 fragment reads per operand per wave per K-step
+  constexpr int QS = 4 / KS;                   // fp32: b128 fragment reads per operand per wave per K-step
+  constexpr int KCW = 2 / KS;                  // split: 16-deep k chunks per wave per K-step
   static_assert(KS == 1 || (KS - 1) * NSUB * 1024 <= STAGE, "split-K partials fit in one stage");
   static_assert(NG % NW == 0, "stage rows must split evenly over the waves");
-  static_assert(KS == 1 || KS == 2 || KS == 4, "KS");
-  static_assert(NS >= 2 && NS <= 6 && GPW * (NS - 2) < 64, "NS");
+  static_assert(KS == 1 || KS == 2 || (!SPLIT && KS == 4), "KS");
+  static_assert(NS >= 2 && NS <= 4 && GPW * (NS - 2) < 64, "NS");
 
   // one __shared__ object per stage: the compiler then sees that a stage being read is
   // not the one being filled and does not drain the in-flight loads before the reads
@@ -121,10 +116,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   __shared__ __attribute__((aligned(16))) float st1[STAGE];
   __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
   __shared__ __attribute__((aligned(16))) float st3[NS > 3 ? STAGE : 4];
-  __shared__ __attribute__((aligned(16))) float st4[NS > 4 ? STAGE : 4];
-  __shared__ __attribute__((aligned(16))) float st5[NS > 5 ? STAGE : 4];
-  float* const stp[6] = {st0, st1, st2, st3, st4, st5};
-  __shared__ int s_next, s_last;
+  float* const stp[4] = {st0, st1, st2, st3};
   __shared__ unsigned red[3][NSUB];
 
   const int tid = threadIdx.x;
@@ -135,203 +127,194 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   const int i = lane & 31, h = lane >> 5;
   const int swz = (i >> 1) & 7;
   const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * wn + i) * 32;
-  const unsigned base = (unsigned)iter * (unsigned)ntiles;
-  // one workgroup per tile (the default grid): no ticket queue, no returning atomic per tile
-  const bool one_each = (int)gridDim.x >= ntiles;
 
-  for (int t = blockIdx.x; t < ntiles;) {
-    const unsigned long long t_tile = __builtin_amdgcn_s_memrealtime();
-    const GemmTile tl = tiles[t];
-    const ProbDesc& p = probs[tl.prob];
-    const int ld = tl.ld, ldm = tl.ldm;
-    const int row0 = tl.tm * BM, col0 = tl.tn * BN;
-    const int nk = tl.nk;
-    // the epilogue's U entries (X = H_T - U), loaded before the first stages so their
-    // latency is spent under the K-loop, not after it (vector loads complete in issue
-    // order: the stage waits below then also cover these)
-    float upre[16];
-    {
-      const int col = col0 + 32 * wn + i;
-      const int colc = col < ld ? col : 0;
+  const GemmTile tl = tiles[blockIdx.x];
+  const ProbDesc& p = probs[tl.prob];
+  const int ld = tl.ld, ldm = tl.ldm;
+  const int row0 = tl.tm * BM, col0 = tl.tn * BN;
+  const int nk = tl.nk;
+  // the epilogue's U entries (X = H_T - U) and, split form, the row / column exponents:
+  // loaded before the first stages so their latency is spent under the K-loop (vector
+  // loads complete in issue order: the stage waits below then also cover these)
+  float upre[16];
+  int epre[16];
+  int ecol = 0;
+  {
+    const int col = col0 + 32 * wn + i;
+    const int colc = col < ld ? col : 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-        upre[r] = ldg(tl.U + (size_t)row * ld + colc);
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      upre[r] = ldg(tl.U + (size_t)row * ld + colc);
+      if (SPLIT) epre[r] = *(__attribute__((address_space(1))) const int*)(tl.eP + row);
     }
-    // per-lane global source of each of this wave's glds pieces (K-step 0)
-    const float* src[GPW];
+    if (SPLIT) ecol = *(__attribute__((address_space(1))) const int*)(tl.eM + colc);
+  }
+  // per-lane global source of each of this wave's glds pieces (K-step 0)
+  const float* src[GPW];
 #pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const int g = wave * GPW + j;
-      const int r = 8 * g + (lane >> 3);                       // image row
-      const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
-      src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + tl.k0 * BK + 4 * c
-                        : tl.M + (size_t)(col0 + r - BM) * ldm + tl.k0 * BK + 4 * c;
-    }
+  for (int j = 0; j < GPW; ++j) {
+    const int g = wave * GPW + j;
+    const int r = 8 * g + (lane >> 3);                       // image row
+    const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+    src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + 4 * c
+                      : tl.M + (size_t)(col0 + r - BM) * ldm + 4 * c;
+  }
 #define ADMMQ_ISSUE(s, kt)                                                 \
   _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
     glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
-    // the first NS-1 stages go out before the stop test, whose inputs (flag, residual
-    // sums) are one dependent read further away; a stopped problem drains them unused
+  // the first NS-1 stages go out before the stop test, whose inputs (flag, residual
+  // sums) are one dependent read further away; a stopped problem drains them unused
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
-    bool skip = p.flags[0] != 0;
-    if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
-      if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
-      skip = true;
-    }
-    if (skip) {
-      wait_vmcnt<0>();   // the speculative stage loads land before the LDS is reused or the wave ends
-      if (tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
-    }
-    if (!skip) {
-      if (tl.first && tl.ks == 0) {   // this iteration's quantizer-search accumulators start at zero
-        unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
-        unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
-        unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
-        for (int c = tid; c < ncand; c += NT) sse[c] = 0ull;
-        for (int c = tid; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
-        if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
-      }
+  for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
+  bool skip = p.flags[0] != 0;
+  if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
+    if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
+    skip = true;
+  }
+  if (skip) {
+    wait_vmcnt<0>();   // the speculative stage loads land before the wave ends
+    return;
+  }
+  if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+    unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
+    unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
+    unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
+    for (int c = tid; c < ncand; c += NT) sse[c] = 0ull;
+    for (int c = tid; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
+    if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
+  }
 
-      f32x16 acc, acc2;
+  f32x16 acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { acc[r] = 0.f; acc2[r] = 0.f; }
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-      // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
-      // stages stay in flight), publish it (barrier), refill the stage consumed one step
-      // ago with K-step kt + NS - 1, multiply. Every step issues exactly GPW loads (past
-      // the end the last K-step is re-read into a stage nobody reads), so the wait count
-      // is one constant and the compiler's own wait tracking stays exact. The main loop
-      // runs whole groups of NS steps (stage static, no branches around the MFMAs, which
-      // would move the accumulators out of AGPRs); the last < NS steps run guarded.
-#define ADMMQ_STEP(s, kt)                                                               \
-  do {                                                                                  \
-    wait_vmcnt<GPW * (NS - 2)>();                                                       \
-    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */ \
-    raw_barrier();                                                                      \
-    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                       \
-    const float* st = stp[s];                                                           \
-    _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                 \
-      const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                              \
-      const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);              \
-      const float4 b = *reinterpret_cast<const float4*>(st + boff + cpos);              \
-      f32x16& ac = (NA == 2 && (qq & 1)) ? acc2 : acc;                                  \
-      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, ac, 0, 0, 0);                 \
-      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, ac, 0, 0, 0);                 \
-      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, ac, 0, 0, 0);                 \
-      ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, ac, 0, 0, 0);                 \
-    }                                                                                   \
+  // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
+  // stages stay in flight), publish it (barrier), refill the stage consumed one step
+  // ago with K-step kt + NS - 1, multiply. Every step issues exactly GPW loads (past
+  // the end the last K-step is re-read into a stage nobody reads), so the wait count
+  // is one constant and the compiler's own wait tracking stays exact. The main loop
+  // runs whole groups of NS steps (stage static, no branches around the MFMAs, which
+  // would move the accumulators out of AGPRs); the last < NS steps run guarded.
+#define ADMMQ_STEP(s, kt)                                                                     \
+  do {                                                                                        \
+    wait_vmcnt<GPW * (NS - 2)>();                                                             \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
+    raw_barrier();                                                                            \
+    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
+    const float* st = stp[s];                                                                 \
+    if constexpr (SPLIT) {                                                                    \
+      _Pragma("unroll") for (int q = 0; q < KCW; ++q) {                                       \
+        const int kc = KCW * ks + q;                                                          \
+        const int ch = ((2 * kc + h) ^ swz) * 4, cl = ((4 + 2 * kc + h) ^ swz) * 4;           \
+        const f16x8 ah = as_h8(*reinterpret_cast<const float4*>(st + aoff + ch));             \
+        const f16x8 al = as_h8(*reinterpret_cast<const float4*>(st + aoff + cl));             \
+        const f16x8 bh = as_h8(*reinterpret_cast<const float4*>(st + boff + ch));             \
+        const f16x8 bl = as_h8(*reinterpret_cast<const float4*>(st + boff + cl));             \
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);                   \
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);                   \
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);                   \
+      }                                                                                       \
+    } else {                                                                                  \
+      _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                     \
+        const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                                  \
+        const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);                  \
+        const float4 b = *reinterpret_cast<const float4*>(st + boff + cpos);                  \
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);                   \
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);                   \
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);                   \
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);                   \
+      }                                                                                       \
+    }                                                                                         \
   } while (0)
-      const int nfull = nk / NS * NS;
-      for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
+  const int nfull = nk / NS * NS;
+  for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) ADMMQ_STEP(s, kt0 + s);
-      }
+    for (int s = 0; s < NS; ++s) ADMMQ_STEP(s, kt0 + s);
+  }
 #pragma unroll
-      for (int s = 0; s < NS - 1; ++s)
-        if (nfull + s < nk) ADMMQ_STEP(s, nfull + s);
+  for (int s = 0; s < NS - 1; ++s)
+    if (nfull + s < nk) ADMMQ_STEP(s, nfull + s);
 #undef ADMMQ_STEP
 #undef ADMMQ_ISSUE
-      // next ticket, drawn once this tile's K-loop is done (its latency hides behind
-      // the epilogue; drawing earlier would hand tiles out before workers are free)
-      if (tid == 0) s_next = one_each ? ntiles : (int)(atomicAdd(queue, 1u) - base) + (int)gridDim.x;
-      __syncthreads();   // nothing in flight any more; the stages may be reused
-      if (NA == 2) {     // the two chains (even / odd fragment groups), summed once
+  __syncthreads();   // nothing in flight any more; the stages may be reused
+  if (KS > 1) {      // fixed-order reduction of the KS partial accumulators (deterministic)
+    if (ks > 0) {
+      float* dst = st0 + ((ks - 1) * NSUB + sub) * 1024;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
-      }
-      if (KS > 1) {      // fixed-order reduction of the KS partial accumulators (deterministic)
-        if (ks > 0) {
-          float* dst = st0 + ((ks - 1) * NSUB + sub) * 1024;
+      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (ks == 0) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
-        }
-        __syncthreads();
-        if (ks == 0) {
+      for (int j = 1; j < KS; ++j) {
+        const float* s2 = st0 + ((j - 1) * NSUB + sub) * 1024;
 #pragma unroll
-          for (int j = 1; j < KS; ++j) {
-            const float* s2 = st0 + ((j - 1) * NSUB + sub) * 1024;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] += s2[r * 64 + lane];
-          }
-        }
-      }
-
-      // split-K pair: publish this half (agent-scope stores write through the XCD L2);
-      // the half whose arrival is second (odd count: two arrivals per pair per launch,
-      // counters zeroed per run) adds the other's partial and runs the epilogue. The
-      // sum of two terms is the same in either arrival order.
-      bool fin = true;
-      if (tl.part >= 0) {
-        float* mine = kpart + ((size_t)tl.part * 2 + tl.ks) * (NSUB * 1024);
-        if (ks == 0) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            __hip_atomic_store(mine + (sub * 16 + r) * 64 + lane, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (tid == 0)
-          s_last = (int)(__hip_atomic_fetch_add(pcnt + tl.part, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u);
-        __syncthreads();
-        fin = s_last != 0;
-        if (fin) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other half's stores are visible
-          if (ks == 0) {
-            const float* other = kpart + ((size_t)tl.part * 2 + (tl.ks ^ 1)) * (NSUB * 1024);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] += ldg(other + (sub * 16 + r) * 64 + lane);
-          }
-        }
-      }
-      // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-      if (ks == 0 && fin) {
-        const int col = col0 + 32 * wn + i;
-        unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
-        if (col < ld) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const size_t off = (size_t)row * ld + col;
-            const float ht = acc[r];
-            const float x = ht - upre[r];
-            p.HT[off] = ht;
-            if (p.X_dbg) p.X[off] = x;   // X = H_T - U is re-formed by its readers; stored for debug output only
-            if (row < p.I && col < p.R) {
-              amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
-              const unsigned e = enc_ord(x);
-              mn = min(mn, e);
-              mxo = max(mxo, e);
-            }
-          }
-        }
-        amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
-        if (lane == 0) { red[0][sub] = amax; red[1][sub] = mn; red[2][sub] = mxo; }
-      }
-      __syncthreads();
-      if (tid == 0 && fin) {
-        unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
-#pragma unroll
-        for (int w = 1; w < NSUB; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
-        unsigned* st = p.mv.stat + 4 * slot;
-        atomicMax(&st[0], a0);
-        atomicMin(&st[1], a1);
-        atomicMax(&st[2], a2);
+        for (int r = 0; r < 16; ++r) acc[r] += s2[r * 64 + lane];
       }
     }
-    if (tid == 0 && t < kTraceMax) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
-      g_gemm_trace[t][0] = t_tile;
-      g_gemm_trace[t][1] = __builtin_amdgcn_s_memrealtime();
-      g_gemm_trace[t][2] = ((unsigned long long)blockIdx.x << 48) | ((unsigned long long)xcc << 32) | hw;
-    }
-    __syncthreads();   // s_next visible; every wave done with this tile's LDS
-    t = s_next;
-    __syncthreads();   // s_next read by all before the next tile's draw overwrites it
   }
+
+  // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if (ks == 0) {
+    const int col = col0 + 32 * wn + i;
+    unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+    if (col < ld) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const size_t off = (size_t)row * ld + col;
+        const float ht = SPLIT ? __builtin_ldexpf(acc[r], -(epre[r] + ecol)) : acc[r];
+        const float x = ht - upre[r];
+        p.HT[off] = ht;
+        if (p.X_dbg) p.X[off] = x;   // X = H_T - U is re-formed by its readers; stored for debug output only
+        if (row < p.I && col < p.R) {
+          amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
+          const unsigned e = enc_ord(x);
+          mn = min(mn, e);
+          mxo = max(mxo, e);
+        }
+      }
+    }
+    amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
+    if (lane == 0) { red[0][sub] = amax; red[1][sub] = mn; red[2][sub] = mxo; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
+#pragma unroll
+    for (int w = 1; w < NSUB; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
+    unsigned* st = p.mv.stat + 4 * slot;
+    atomicMax(&st[0], a0);
+    atomicMin(&st[1], a1);
+    atomicMax(&st[2], a2);
+  }
+}
+
+// One block per (problem, row): rows [0, Ip) of P (fp32, padded, zero pads) -> P2 / eP.
+// `which` 0: P of every split problem; 1: M (rows [0, ldm)) -> M2 / eM.
+__global__ __launch_bounds__(256) void k_split_rows(const ProbDesc* __restrict__ probs, int which) {
+  const ProbDesc& p = probs[blockIdx.y];
+  if (!p.split) return;
+  const int nrows = which ? p.ldm : p.Ip;
+  const int row = blockIdx.x;
+  if (row >= nrows) return;
+  const int n = which ? p.ldm : p.ld;
+  const float* src = (which ? p.M : p.P) + (size_t)row * n;
+  _Float16* dst = (which ? p.M2 : p.P2) + (size_t)row * 2 * n;
+  float m = 0.f;
+  for (int c = 4 * threadIdx.x; c < n; c += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(src + c);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  m = __uint_as_float(wave_max_u32(__float_as_uint(m)));
+  __shared__ unsigned wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = __float_as_uint(m);
+  __syncthreads();
+  const float amax = __uint_as_float(max(max(wm[0], wm[1]), max(wm[2], wm[3])));
+  const int e = split_exponent(amax);
+  for (int c = 4 * threadIdx.x; c < n; c += 1024) split_store4(dst, c, *reinterpret_cast<const float4*>(src + c), e);
+  if (threadIdx.x == 0) (which ? p.eM : p.eP)[row] = e;
 }
 
 // ---------------------------------------------------------------------------
@@ -347,10 +330,6 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
 // write through the XCD L2), the last block to arrive (per-column-block counter)
 // sums the nkg partials in kg order and runs the epilogue. Every sum is in a fixed
 // order: the result does not depend on which block arrives last.
-// Per-block timeline of the last thin launch (diagnostics: admmq_debug_thin_trace):
-// s_memrealtime at {start, loads of P/U/stop test in, FMA done, end} and {last-arriver, xcc}
-__device__ unsigned long long g_thin_trace[4096][5];
-
 template <int NR>
 __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ probs,
                                                    const ThinUnit* __restrict__ units, int slot, int iter,
@@ -362,7 +341,6 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
   __shared__ __attribute__((aligned(16))) float Pt[kThinK][PS];
   __shared__ __attribute__((aligned(16))) float red[4][NR][kThinCols];
   __shared__ int s_last;
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   const ThinUnit u = units[blockIdx.x];
   const ProbDesc& p = probs[u.prob];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -401,7 +379,6 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
   }
   wait_vmcnt<32>();   // P, flag, residuals and U are in; the 32 M rows stay in flight
   __builtin_amdgcn_sched_barrier(0);   // nothing that reads them is scheduled above the wait
-  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   if (done) return;
   if (iter > 0) {   // stop test (source/admm.py:59-65), uniform over the problem's units
     double t = rv;
@@ -440,7 +417,6 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
       acc[i][1] = __builtin_elementwise_fma(mzw, pp, acc[i][1]);
     }
   }
-  const unsigned long long t_fma = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int i = 0; i < NR; ++i)
     *reinterpret_cast<float4*>(&red[wave][i][4 * lane]) = make_float4(acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y);
@@ -495,14 +471,7 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
       s_last = last;
     }
     __syncthreads();
-    if (!s_last) {
-      if (tid == 0 && blockIdx.x < 4096) {
-        g_thin_trace[blockIdx.x][0] = t_start; g_thin_trace[blockIdx.x][1] = t_in;
-        g_thin_trace[blockIdx.x][2] = t_fma; g_thin_trace[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
-        g_thin_trace[blockIdx.x][4] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));
-      }
-      return;
-    }
+    if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' partials are visible
     // sum the nkg partials in kg order, 8 reduction blocks' loads in flight at a time
 #pragma unroll
@@ -561,89 +530,30 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
     atomicMin(&st[1], mn);
     atomicMax(&st[2], mxo);
   }
-  if (tid == 0 && blockIdx.x < 4096) {
-    g_thin_trace[blockIdx.x][0] = t_start; g_thin_trace[blockIdx.x][1] = t_in;
-    g_thin_trace[blockIdx.x][2] = t_fma; g_thin_trace[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
-    g_thin_trace[blockIdx.x][4] = (1ull << 32) | __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));
-  }
 }
 
-int copy_thin_trace(unsigned long long* host, int n) {
-  n = n < 4096 ? n : 4096;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_thin_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess ? n : -1;
+void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s) {
+  if (nprob > 0 && maxrows > 0) hipLaunchKernelGGL(k_split_rows, dim3(maxrows, nprob), dim3(256), 0, s, d, which);
 }
 
-int copy_gemm_trace(unsigned long long* host, int n) {
-  n = n < kTraceMax ? n : kTraceMax;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), (size_t)n * 3 * sizeof(unsigned long long)) == hipSuccess ? n : -1;
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
-// Row height of the big tiles / 32 (the padded factor height Ip is a multiple of it)
-int gemm_big_wm() {
-  static const int wm = env_int("ADMMQ_GEMM_WM", 2) == 4 ? 4 : 2;
-  return wm;
-}
-
-// Workgroups per CU for the persistent grid (MI355X: 256 CUs)
-static int gemm_grid(int ntiles, int per_cu) { return std::min(ntiles, 256 * per_cu); }
-
-// Persistent GEMM grid: workgroups per CU drawing tiles from the ticket queue (0: one
-// workgroup per tile).
-int gemm_persistent_per_cu() {
-  static const int v = env_int("ADMMQ_GEMM_PER_CU", 0);
-  return v;
-}
-
-// Tiles with at least this many K-steps are split into two K halves (0: never).
-int gemm_split_min_steps() {
-  static const int v = env_int("ADMMQ_GEMM_SPLIT", 0);
-  return v;
-}
-
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, unsigned* queue,
-                 float* kpart, unsigned* pcnt, int slot, int iter, float eps, int ncand, hipStream_t s) {
-  // tiles[0 .. ntiles_big) are (32 WM)x64, then ntiles_small 32x64 tiles (WM=1);
-  // queue[0] / queue[1] are their ticket counters.
-  static const int cfg_big = env_int("ADMMQ_GEMM_BIG", 13);     // KS*10 + NS
-  static const int cfg_small = env_int("ADMMQ_GEMM_SMALL", 24);
-  const int per_cu = gemm_persistent_per_cu();                    // 0: one workgroup per tile
-#define ADMMQ_GEMM(WM, KS, NS, n, t, q)                                                                      \
-  hipLaunchKernelGGL((k_gemm<WM, KS, NS>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, d, \
-                     t, n, q, kpart, pcnt, slot, iter, eps, ncand)
-#define ADMMQ_GEMM2(WM, KS, NS, n, t, q)                                                                     \
-  hipLaunchKernelGGL((k_gemm<WM, KS, NS, 2>), dim3(per_cu ? gemm_grid(n, per_cu) : n), dim3(128 * WM * KS), 0, s, \
-                     d, t, n, q, kpart, pcnt, slot, iter, eps, ncand)
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
+                 int iter, float eps, int ncand, hipStream_t s) {
+  // tiles[0 .. ntiles_big) are 64x64 (WM = 2, one wave per 32x32 sub-tile, 3-deep ring),
+  // then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors, 2 waves per sub-tile
+  // splitting each K-step, 4-deep ring)
   if (ntiles_big > 0) {
-    if (gemm_big_wm() == 4) {
-      ADMMQ_GEMM(4, 1, 3, ntiles_big, tiles, queue);
-    } else {
-      switch (cfg_big) {
-        case 14: ADMMQ_GEMM(2, 1, 4, ntiles_big, tiles, queue); break;
-        case 113: ADMMQ_GEMM2(2, 1, 3, ntiles_big, tiles, queue); break;
-        case 114: ADMMQ_GEMM2(2, 1, 4, ntiles_big, tiles, queue); break;
-        case 15: ADMMQ_GEMM(2, 1, 5, ntiles_big, tiles, queue); break;
-        case 16: ADMMQ_GEMM(2, 1, 6, ntiles_big, tiles, queue); break;
-        case 24: ADMMQ_GEMM(2, 2, 4, ntiles_big, tiles, queue); break;
-        case 23: ADMMQ_GEMM(2, 2, 3, ntiles_big, tiles, queue); break;
-        case 12: ADMMQ_GEMM(2, 1, 2, ntiles_big, tiles, queue); break;
-        default: ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles, queue); break;
-      }
-    }
+    if (split)
+      hipLaunchKernelGGL((k_gemm<2, 1, 3, true>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
+    else
+      hipLaunchKernelGGL((k_gemm<2, 1, 3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
   }
   if (ntiles_small > 0) {
     const GemmTile* t = tiles + ntiles_big;
-    switch (cfg_small) {
-      case 14: ADMMQ_GEMM(1, 1, 4, ntiles_small, t, queue + 1); break;
-      default: ADMMQ_GEMM(1, 2, 4, ntiles_small, t, queue + 1); break;
-    }
+    if (split)
+      hipLaunchKernelGGL((k_gemm<1, 2, 4, true>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
+    else
+      hipLaunchKernelGGL((k_gemm<1, 2, 4, false>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
   }
-#undef ADMMQ_GEMM
-#undef ADMMQ_GEMM2
 }
 
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,

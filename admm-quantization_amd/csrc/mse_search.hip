@@ -235,7 +235,7 @@ __device__ void select_wave(const MseView& v, int* sel, int* lsel, const unsigne
     if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
     else { sel[0] = total; sel[1] = 0; }
     lsel[0] = sel[0]; lsel[1] = sel[1];
-    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+    if (ADMMQ_TRACE) atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
   }
 }
 
@@ -276,7 +276,7 @@ __device__ void sse_in_block(const MseView& v, const int* lsel, int ncand, int b
 template <int QMAX, int NV>
 __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
                                                    const Chunk* __restrict__ chunks, int ncand, int slot, int abl) {
-  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T0 = ADMMQ_NOW();
   const Chunk ck = chunks[blockIdx.x];
   const MseView& v = mview(d, qj, ck.job);
   if (v.done && *v.done) return;
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   if (abl & 32) { __syncthreads(); fill_thresholds(thr, mx, n, QMAX, blockDim.x); }
   for (int b = threadIdx.x; b < nb; b += blockDim.x) { h1[b] = 0ull; h2[b] = 0u; }
   __syncthreads();
-  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T1 = ADMMQ_NOW();
   const float S0 = (float)(0.2 * (double)mx);
   const float E0 = (float)(1.2 * (double)mx);
   const float inv_step = (n > 1) ? (float)(n - 1) / (E0 - S0) : 0.f;
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
     if (full2) atomicAdd(&h2[n], full2);
   }
   __syncthreads();
-  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T2 = ADMMQ_NOW();
   const int rep = blockIdx.x & (kHistRep - 1);
   unsigned long long* g1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
   unsigned long long* g2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
@@ -405,9 +405,9 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
     last = (__hip_atomic_fetch_add(&v.ticket[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             (unsigned)(v.nhist - 1)) ? 1 : 0;
   __syncthreads();
-  const unsigned long long T3 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T3 = ADMMQ_NOW();
   auto trace = [&](unsigned long long T4) {
-    if (threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
+    if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
       g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = T1; g_hist_trace[blockIdx.x][2] = T2;
       g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4;
       g_hist_trace[blockIdx.x][5] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   }
   __syncthreads();
   sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
-  trace(__builtin_amdgcn_s_memrealtime());
+  trace(ADMMQ_NOW());
 }
 
 // ---------------------------------------------------------------------------
@@ -511,7 +511,7 @@ __device__ void select_wave2(const MseView& v, int* sel, int* lsel, const unsign
     if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
     else { sel[0] = total; sel[1] = 0; }
     lsel[0] = sel[0]; lsel[1] = sel[1];
-    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+    if (ADMMQ_TRACE) atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
   }
 }
 
@@ -552,7 +552,7 @@ __device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned lon
     if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
     else { sel[0] = total; sel[1] = 0; }
     lsel[0] = sel[0]; lsel[1] = sel[1];
-    atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+    if (ADMMQ_TRACE) atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
   }
   __syncthreads();
 }
@@ -615,9 +615,9 @@ int copy_small_trace(unsigned long long* host, int n) {
              ? n : -1;
 }
 #define ADMMQ_SMALL_STAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+  if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][k] = ADMMQ_NOW()
 #define ADMMQ_SETUP_STAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < kSetupTraceMax) g_setup_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+  if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kSetupTraceMax) g_setup_trace[blockIdx.x][k] = ADMMQ_NOW()
 
 // The global inputs of the stage-1 table setup that do not depend on max|x|: this
 // thread's entries of the host order of the thresholds (blocks of >= 512 threads) and
@@ -906,7 +906,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
                                                       const Chunk* __restrict__ chunks, int ncand, int slot,
                                                       const unsigned short* __restrict__ rank0,
                                                       const unsigned short* __restrict__ groups, int ngroups) {
-  const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T0 = ADMMQ_NOW();
   const Chunk ck = chunks[blockIdx.x];
   // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
   // the threshold order, this thread's elements - all issued before any is used
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
   const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell, kH3Threads);
-  const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T1 = ADMMQ_NOW();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
 #pragma unroll
@@ -972,7 +972,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
     h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
   }
   __syncthreads();
-  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T2 = ADMMQ_NOW();
   h3_suffix<kH3Threads, 4>(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
   // per-candidate totals of this block into one of kHistRep replicas
   const int rep = blockIdx.x & (kHistRep - 1);
@@ -1001,9 +1001,9 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
     last = (__hip_atomic_fetch_add(&v.ticket[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             (unsigned)(v.nhist - 1)) ? 1 : 0;
   __syncthreads();
-  const unsigned long long T3 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long T3 = ADMMQ_NOW();
   auto trace = [&](unsigned long long T4) {
-    if (threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
+    if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
       g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = T1; g_hist_trace[blockIdx.x][2] = T2;
       g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4; g_hist_trace[blockIdx.x][5] = 0;
     }
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
                                         __HIP_MEMORY_SCOPE_AGENT);
     select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
     sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
-    trace(__builtin_amdgcn_s_memrealtime());
+    trace(ADMMQ_NOW());
     return;
   }
   unsigned long long* T1v = sumA;                 // reuse LDS: n each
@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   }
   __syncthreads();
   sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
-  trace(__builtin_amdgcn_s_memrealtime());
+  trace(ADMMQ_NOW());
 }
 
 // Small ADMM jobs (thin factors, I <= kThinRows: the 9-row spatial mode of a 3x3 conv,
@@ -1146,7 +1146,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
     for (int k = 0; k < nw; ++k) S2 += red[k];
     select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
     ADMMQ_SMALL_STAMP(5);
-    if (threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][8] = (unsigned)lsel[0];
+    if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kSmallTraceMax) g_small_trace[blockIdx.x][8] = (unsigned)lsel[0];
     sse_in_block(v, lsel, n, bits, slot, mx, reinterpret_cast<float4*>(smem));
     __syncthreads();
     ADMMQ_SMALL_STAMP(6);
@@ -1320,7 +1320,7 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
                      int slot, int nv, hipStream_t s) {
   if (nchunks <= 0) return;
   const size_t lds = hist_lds_bytes(ncand, bits);
-  static const int abl = getenv("ADMMQ_HIST_ABLATE") ? atoi(getenv("ADMMQ_HIST_ABLATE")) : 0;   // timing only
+  const int abl = 0;
 #define ADMMQ_H1(Q, V) \
   hipLaunchKernelGGL((k_mse_hist<Q, V>), dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl)
 #define ADMMQ_H1N(Q) if (nv == 2) ADMMQ_H1(Q, 2); else ADMMQ_H1(Q, 1)

@@ -285,4 +285,30 @@ __device__ __forceinline__ QParams block_qparams(int scheme, int bits, const Mse
   return qparams_stats(scheme, bits, dec_ord(stat[1]), dec_ord(stat[2]), has_nan ? 1 : 0, has_kw, kw_min, kw_max);
 }
 
+// ---------------------------------------------------------------------------
+// Split operand planes (kSolveSplit). A row of n values (n a multiple of 32) becomes
+// n/32 blocks of [32 hi halfs][32 lo halfs] (the fp32 row's bytes) with the row's
+// exponent e = 14 - floor(log2 max|x|) (max|x| 2^e in [2^14, 2^15): no fp16 overflow):
+//   hi = fp16(x 2^e), lo = fp16(x 2^e - hi)   (x 2^e and the difference are exact in fp32)
+__device__ __forceinline__ int split_exponent(float amax) {
+  if (!(amax > 0.f) || !(amax < __builtin_inff())) return 0;
+  int e;
+  (void)__builtin_frexpf(amax, &e);   // amax = m 2^e, m in [0.5, 1): floor(log2 amax) = e - 1
+  return 15 - e;
+}
+__device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 v, int e) {
+  const float s[4] = {__builtin_ldexpf(v.x, e), __builtin_ldexpf(v.y, e), __builtin_ldexpf(v.z, e),
+                      __builtin_ldexpf(v.w, e)};
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  h4 hi, lo;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hi[k] = (_Float16)s[k];
+    lo[k] = (_Float16)(s[k] - (float)hi[k]);
+  }
+  _Float16* b = dst_row + (col >> 5) * 64 + (col & 31);
+  *reinterpret_cast<h4*>(b) = hi;
+  *reinterpret_cast<h4*>(b + 32) = lo;
+}
+
 }  // namespace admmq

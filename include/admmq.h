@@ -105,6 +105,15 @@ int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t 
  * be the argmin). Both return bit-identical results. */
 int32_t admmq_set_exhaustive_search(int32_t enable);
 
+/* Operand form of the per-iteration solve H_T = P M (the cholesky_solve of
+ * source/admm.py:56): 1 (default) = split fp16 planes on f16 MFMA (P and M as
+ * hi + lo fp16 with a power-of-two exponent per row, 3 products, fp32 accumulation;
+ * about 2^-21 relative per product), 0 = fp32 MFMA. Both stay within the 1e-5
+ * rel-Frobenius solve contract of SURVEY.md §8(c) P2. Process-wide; read at
+ * admmq_admm_prepare / _run (a prepare and its runs must see the same mode). */
+int32_t admmq_set_solve_mode(int32_t mode);
+int32_t admmq_get_solve_mode(void);
+
 /* Optional HIP-event timing of every launch class issued by admmq_admm_prepare/run on
  * this thread between begin and end: class 0 GEMM (solve), 1 MSE candidate sweep,
  * 2 projection/dual update, 3 whole prepare phase. Only ADMM iterations it with

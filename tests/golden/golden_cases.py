@@ -101,3 +101,34 @@ def canonical_sha(a) -> str:
     u = a.view(np.uint32)
     u[np.isnan(a)] = np.uint32(0x7FC00000)
     return hashlib.sha256(u.tobytes()).hexdigest()
+
+
+def grid_levels(H):
+    """(levels, scale) of a tensor on a uniform quantization grid: H = fl32(k * s) with
+    integer k. s is the smallest positive |H| (some element has |k| = 1 on every real
+    factor; checked: every element must then reproduce as k * s)."""
+    H = np.asarray(H, np.float32)
+    a = np.abs(H[np.isfinite(H)])
+    pos = a[a > 0]
+    if pos.size == 0:
+        return np.zeros(H.shape, np.int64), np.float32(0)
+    s = np.float32(pos.min())
+    k = np.rint(H.astype(np.float64) / np.float64(s))
+    if not np.array_equal((k.astype(np.float32) * s).astype(np.float32), H):
+        return None, s
+    return k.astype(np.int64), s
+
+
+def level_mismatch(H, H_ref, X, half_window=1e-4):
+    """P2 of SURVEY §8(c): compare the integer levels of two quantized factors.
+    Returns (n_mismatch, n_unexplained): mismatches, and those NOT explained by a
+    near-half rounding of X (|X/s - (k + 1/2)| < half_window with our own scale s),
+    or None when either tensor is not on a uniform grid (the scheme is affine)."""
+    k, s = grid_levels(H)
+    kr, sr = grid_levels(H_ref)
+    if k is None or kr is None:
+        return None
+    bad = k != kr
+    y = np.asarray(X, np.float64) / np.float64(s)
+    near = np.abs(np.abs(y - np.floor(y)) - 0.5) < half_window
+    return int(bad.sum()), int((bad & ~(near & (np.abs(k - kr) == 1))).sum())

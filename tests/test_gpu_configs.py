@@ -1,0 +1,162 @@
+"""Per-config GPU tests: BASELINE.json configs C3 (resnet18, all 16 3x3 convs in ONE
+batched call), C4 (resnet50, all 48 convs: 16 3-way + 32 2-way, R 16..1141) and C5
+(Llama-7B 2-way shapes (4096,4096) R=1024 and (11008,4096) R=1492).
+
+For every problem of a config, one batched ADMM step (both solve forms):
+  * H_T within 1e-5 rel-Frobenius of the CPU oracle (scipy float32 Cholesky, the
+    reference's formulation; C5: an fp64 solve);
+  * the projection bit-exact: the oracle quantizer (oracle/quant_oracle_c.c) applied to
+    the kernel's own X = H_T - U equals the kernel's H;
+  * the dual update bit-exact: U = U0 + (H - H_T);
+and, over 3 inner iterations, the batched call equals per-problem calls bit-for-bit.
+Inputs: synthetic weights of the configs' shapes (admmq.synthetic), seed-42 random init,
+F/G from the oracle's Gram/MTTKRP (C5: torch matmuls).
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from oracle import admm_oracle as ao
+from oracle import quant_oracle_c as qc
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+MSE = "tensor_mseminmax_symmetric"
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+def _t(torch, dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _config_problems(model, mode):
+    """[(name, H0, F, G)] for `mode` of every layer of `model` that has that mode."""
+    import torch
+    from admmq import synthetic
+    out = []
+    for l, s in enumerate(synthetic.MODELS[model]()):
+        if mode >= len(s.shape):
+            continue
+        W = synthetic.layer_weight(s, l)
+        R = s.rank()
+        g = torch.Generator().manual_seed(42)
+        fs = [torch.randn(n, R, generator=g).numpy() for n in W.shape]
+        G, F = ao.gram_mttkrp(W, fs, mode)
+        out.append((s.name, fs[mode], F, G))
+    return out
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _check_step(torch, dev, probs, solve, ref_solver):
+    from admmq import admm_iteration_batched
+    from admmq._lib import solve_mode
+    rng = np.random.default_rng(9)
+    U0s = [(rng.standard_normal(H.shape) * 1e-3).astype(np.float32) for (_, H, _, _) in probs]
+    ps = [(_t(torch, dev, H), _t(torch, dev, U0), _t(torch, dev, F), _t(torch, dev, G))
+          for (_, H, F, G), U0 in zip(probs, U0s)]
+    with solve_mode(solve):
+        Hs, dbg = admm_iteration_batched(ps, 2, 1e-8, 4, MSE, debug_outputs=True)
+    worst = 0.0
+    for (name, H0, F, G), U0, H, (HT, X), p in zip(probs, U0s, Hs, dbg, ps):
+        HT, X, H, U = HT.cpu().numpy(), X.cpu().numpy(), H.cpu().numpy(), p[1].cpu().numpy()
+        ref = ref_solver(H0, U0, F, G)
+        rel = _rel(HT, ref)
+        worst = max(worst, rel)
+        assert rel < 1e-5, (name, rel)
+        assert np.array_equal(_bits(X), _bits((HT - U0).astype(np.float32))), name
+        Hq, _ = qc.quantize_mse(X, 4)
+        assert np.array_equal(_bits(H), _bits(Hq)), name
+        assert np.array_equal(_bits(U), _bits((U0 + (Hq - HT).astype(np.float32)).astype(np.float32))), name
+    return worst
+
+
+def _oracle_ht(H0, U0, F, G):
+    _, _, info = ao.admm_iteration(H0, U0, F, G, 2, 1e-8, 4, MSE, return_info=True)
+    return info["HT"]
+
+
+def _batched_equals_single(torch, dev, probs, iters=4):
+    from admmq import admm_iteration_batched
+    mk = lambda: [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))  # noqa
+                  for (_, H, F, G) in probs]
+    ps = mk()
+    Hs = admm_iteration_batched(ps, iters, 0.0, 4, MSE)
+    for k, (p, H) in enumerate(zip(ps, Hs)):
+        q = mk()[k]
+        (H1,) = admm_iteration_batched([q], iters, 0.0, 4, MSE)
+        assert np.array_equal(_bits(H.cpu().numpy()), _bits(H1.cpu().numpy())), probs[k][0]
+        assert np.array_equal(_bits(p[1].cpu().numpy()), _bits(q[1].cpu().numpy())), probs[k][0]
+
+
+@pytest.mark.parametrize("solve", ["split", "fp32"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_c3_resnet18_all_layers(torch_dev, mode, solve):
+    torch, dev = torch_dev
+    probs = _config_problems("resnet18", mode)
+    assert len(probs) == 16
+    worst = _check_step(torch, dev, probs, solve, _oracle_ht)
+    print(f"C3 mode {mode} {solve}: worst H_T rel {worst:.2e}")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_c3_batched_equals_single(torch_dev, mode):
+    torch, dev = torch_dev
+    _batched_equals_single(torch, dev, _config_problems("resnet18", mode))
+
+
+@pytest.mark.parametrize("solve", ["split", "fp32"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_c4_resnet50_all_layers(torch_dev, mode, solve):
+    torch, dev = torch_dev
+    probs = _config_problems("resnet50", mode)
+    assert len(probs) == (48 if mode < 2 else 16)
+    worst = _check_step(torch, dev, probs, solve, _oracle_ht)
+    print(f"C4 mode {mode} {solve}: {len(probs)} problems, worst H_T rel {worst:.2e}")
+
+
+def test_c4_batched_equals_single(torch_dev):
+    torch, dev = torch_dev
+    probs = _config_problems("resnet50", 0)
+    _batched_equals_single(torch, dev, probs[::3], iters=3)
+
+
+def _llama_problem(torch, dev, I, J, R, seed):
+    """2-way mode 0 of W (I, J): F = W B, G = B^T B (scripts/factorize.py:276-277)."""
+    g = torch.Generator().manual_seed(seed)
+    W = (torch.randn(I, J, generator=g) * 0.02).to(dev)
+    A = torch.randn(I, R, generator=g).to(dev)
+    B = torch.randn(J, R, generator=g).to(dev)
+    return A, W @ B, B.T @ B
+
+
+def _fp64_ht(H0, U0, F, G):
+    import scipy.linalg as sla
+    R = G.shape[0]
+    rho = np.float32(np.float32(np.sum(np.diag(G).astype(np.float64))) / np.float32(R))
+    A = G.astype(np.float64) + float(rho) * np.eye(R)
+    P = F.astype(np.float64) + float(rho) * (H0.astype(np.float64) + U0.astype(np.float64))
+    return sla.cho_solve(sla.cho_factor(A, lower=True), P.T).T
+
+
+@pytest.mark.parametrize("solve", ["split", "fp32"])
+@pytest.mark.parametrize("I,J,R", [(4096, 4096, 1024), (11008, 4096, 1492)])
+def test_c5_llama_shapes(torch_dev, I, J, R, solve):
+    torch, dev = torch_dev
+    A, F, G = _llama_problem(torch, dev, I, J, R, seed=I + R)
+    probs = [("llama", A.cpu().numpy(), F.cpu().numpy(), G.cpu().numpy())]
+    worst = _check_step(torch, dev, probs, solve, _fp64_ht)
+    print(f"C5 ({I},{J}) R={R} {solve}: H_T rel vs fp64 {worst:.2e}")

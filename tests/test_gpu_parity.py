@@ -165,15 +165,18 @@ def _layer_problem(layer="layer1.0.conv1", mode=0, seed=42):
                                         ("layer2.0.conv1", 0), ("layer3.0.conv2", 1), ("layer4.0.conv2", 0),
                                         ("layer4.0.conv2", 2)])
 @pytest.mark.parametrize("qscheme", [MSE, "tensor_minmax", "tensor_symmetric", "tensor_affine"])
-def test_one_step_stagewise(torch_dev, layer, mode, qscheme):
+@pytest.mark.parametrize("solve", ["split", "fp32"])
+def test_one_step_stagewise(torch_dev, layer, mode, qscheme, solve):
     torch, dev = torch_dev
     from admmq import admm_iteration_batched
+    from admmq._lib import solve_mode
     H0, F, G = _layer_problem(layer, mode)
     rng = np.random.default_rng(5)
     U0 = (rng.standard_normal(H0.shape) * 0.01).astype(np.float32)
     U = _t(torch, dev, U0)
-    (H,), dbg = admm_iteration_batched([(_t(torch, dev, H0), U, _t(torch, dev, F), _t(torch, dev, G))], 2, 1e-8, 4,
-                                       qscheme, debug_outputs=True)
+    with solve_mode(solve):
+        (H,), dbg = admm_iteration_batched([(_t(torch, dev, H0), U, _t(torch, dev, F), _t(torch, dev, G))], 2, 1e-8,
+                                           4, qscheme, debug_outputs=True)
     HT, X = (a.cpu().numpy() for a in dbg[0])
     _, _, info = ao.admm_iteration(H0, U0, F, G, 2, 1e-8, 4, qscheme, return_info=True)
     assert _rel(HT, info["HT"]) < 1e-5                      # the solve

@@ -543,7 +543,7 @@ int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class) {
   if (!g_prof.on) return fail(ADMMQ_ERR_ARG, "profiling not active");
   g_prof.on = false;
   g_prof.sampled = true;
-  for (int c = 0; c < 4; ++c) { ms_per_class[c] = 0.0; launches_per_class[c] = 0; }
+  for (int c = 0; c < ADMMQ_PROF_CLASSES; ++c) { ms_per_class[c] = 0.0; launches_per_class[c] = 0; }
   const size_t pairs = std::min(g_prof.next / 2, g_prof.cls.size());
   int rc = ADMMQ_OK;
   if (pairs > 0 && hipEventSynchronize(g_prof.ev[2 * pairs - 1]) != hipSuccess) rc = fail(ADMMQ_ERR_HIP, "sync");
@@ -575,7 +575,7 @@ int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t nu
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if ((rc = upload_admm(pl, s))) return rc;
-  prof_class(3); prof_mark(s);
+  prof_class(ADMMQ_PROF_PREPARE); prof_mark(s);
   launch_rho(pl.d_desc, nprob, s);
   launch_pack(pl.d_desc, nprob, pl.maxIp, pl.maxld, s);
   launch_fill_a64(pl.d_desc, nprob, pl.maxldm, s);
@@ -618,31 +618,50 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
-    prof_class(0); prof_mark(s);
-    launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps, num_attempts, s);
-    launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
-    prof_mark(s);
-    if (qscheme == kMse) {
-      prof_class(1); prof_mark(s);
-      // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
-      if (!exhaustive && merged) {
-        launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, fuse_small ? pl.nhist_big : nhist, num_attempts, bits, slot,
-                         pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, s);
-        if (fuse_small)   // the small jobs' search and finalize in one block each
-          launch_mse_small_admm(pl.d_desc, pl.d_small, (int)pl.small.size(), pl.small_groups, num_attempts, bits,
-                                slot, it, pl.d_rank0, pl.d_groups, ngroups, s);
-      } else if (!exhaustive) {
-        launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.hist_nv, s);
-      } else {
-        launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
-        launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
-      }
+    // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
+    if (pl.ntiles_small + pl.ntiles_big > 0) {
+      prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
+      launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps, num_attempts, s);
       prof_mark(s);
     }
-    prof_class(2); prof_mark(s);
-    launch_finalize_admm(pl.d_desc, pl.d_fin, fuse_small ? pl.nfin_big : nfin, pl.fin_groups, num_attempts, bits,
-                         qscheme, slot, it, s);
-    prof_mark(s);
+    if (!pl.thin.empty()) {
+      prof_class(ADMMQ_PROF_GEMM_THIN); prof_mark(s);
+      launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
+      prof_mark(s);
+    }
+    if (qscheme == kMse) {
+      // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
+      if (!exhaustive && merged) {
+        const int nh = fuse_small ? pl.nhist_big : nhist;
+        if (nh > 0) {
+          prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
+          launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, nh, num_attempts, bits, slot, pl.d_rank0, pl.d_groups,
+                           ngroups, pl.hist_nv, s);
+          prof_mark(s);
+        }
+        if (fuse_small) {   // the small jobs' search and finalize in one block each
+          prof_class(ADMMQ_PROF_SMALL); prof_mark(s);
+          launch_mse_small_admm(pl.d_desc, pl.d_small, (int)pl.small.size(), pl.small_groups, num_attempts, bits,
+                                slot, it, pl.d_rank0, pl.d_groups, ngroups, s);
+          prof_mark(s);
+        }
+      } else {
+        prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
+        if (!exhaustive) {
+          launch_mse_hist(pl.d_desc, nullptr, pl.d_hist, nhist, num_attempts, bits, slot, pl.hist_nv, s);
+        } else {
+          launch_mse_select_all(pl.d_desc, nullptr, nprob, num_attempts, slot, s);
+          launch_mse_sse(pl.d_desc, nullptr, pl.d_sse, nsse, num_attempts, bits, slot, s);
+        }
+        prof_mark(s);
+      }
+    }
+    const int nf = fuse_small ? pl.nfin_big : nfin;
+    if (nf > 0) {
+      prof_class(ADMMQ_PROF_FINALIZE); prof_mark(s);
+      launch_finalize_admm(pl.d_desc, pl.d_fin, nf, pl.fin_groups, num_attempts, bits, qscheme, slot, it, s);
+      prof_mark(s);
+    }
   }
   g_prof.sampled = true;
   if (max_iter > 1) launch_unpack(pl.d_desc, nprob, pl.maxI, pl.maxR, s);

@@ -9,11 +9,11 @@ iterations, eps=0 so no early exit), the re-quantization, then the two
 reconstruction errors. Unit: factor-iterations/s (one execution of the loop body
 source/admm.py:56-65 on one (layer, mode) factor); 47,952 per step per GPU.
 
-Multi-GPU (one process per GPU, torchrun): every rank factorizes its own resnet18
-weight set (replica r: seeds 1000+l+100r) - weak scaling, no data-path collective
-- and the converged factors are gathered to rank 0 with one RCCL gather per step.
-`--shard layers` instead splits ONE model's layers over the ranks (LPT; strong
-scaling, capped by the largest layer - SURVEY §8(e)).
+Multi-GPU (one process per GPU, torchrun): the default `--shard layers`
+splits ONE model's layers over the ranks by LPT on layer cost (strong scaling, capped
+by the largest layer: the line reports the cap), no data-path collective, and the
+converged factors are gathered to rank 0 with one RCCL gather per step. `--shard
+replica` instead gives every rank its own weight set (seeds 1000+l+100r, weak scaling).
 """
 from __future__ import annotations
 
@@ -67,15 +67,15 @@ def workload_name(model, work, max_iter_admm):
 
 
 def build_workload(model, rank, world, shard, device):
+    """This rank's layers (LPT over layer cost when sharding), their
+    synthetic weights and seed-42 random init, plus the static shard plan: every rank's
+    factor element count (so the final gather needs no size exchange) and the LPT
+    load-imbalance cap on the speedup."""
     from admmq import synthetic
     specs = synthetic.MODELS[model]()
-    if shard == "layers" and world > 1:
-        own = lpt(specs, world)
-        mine = [i for i in range(len(specs)) if own[i] == rank]
-        replica = 0
-    else:
-        mine = list(range(len(specs)))
-        replica = rank
+    owner = lpt(specs, world) if (shard == "layers" and world > 1) else {i: rank for i in range(len(specs))}
+    mine = [i for i in range(len(specs)) if owner[i] == rank]
+    replica = rank if shard == "replica" else 0
     work = []
     for i in mine:
         s = specs[i]
@@ -84,7 +84,20 @@ def build_workload(model, rank, world, shard, device):
         g = torch.Generator().manual_seed(42)
         init = [torch.randn(n, R, generator=g).to(device) for n in s.shape]
         work.append((s, W, R, init))
-    return work
+    numel = [0] * world
+    loads = [0.0] * world
+    for i, s in enumerate(specs):
+        for k in (range(world) if shard == "replica" else [owner[i]]):
+            numel[k] += sum(n * s.rank() for n in s.shape)
+            loads[k] += layer_cost(s, s.rank())
+    total = sum(layer_cost(s, s.rank()) for s in specs)
+    info = None
+    if shard == "layers":
+        info = {"policy": "LPT over whole layers, cost sum_m (2 I_m R^2 + 1600 I_m R) (SURVEY §8(e))",
+                "layers_per_rank": [sum(1 for i in owner if owner[i] == k) for k in range(world)],
+                "lpt_speedup_cap": total / max(loads),
+                "whole_layer_speedup_cap": total / max(layer_cost(s, s.rank()) for s in specs)}
+    return work, numel, info
 
 
 def run_step(work, max_iter_admm, num_attempts=200):
@@ -94,19 +107,19 @@ def run_step(work, max_iter_admm, num_attempts=200):
     return runs
 
 
-def gather_factors(runs, rank, world, device):
+def gather_factors(runs, rank, world, numel, device):
+    """The single collective of the path: every rank's converged factors to rank 0 (one
+    RCCL gather over xGMI). Sizes are static (numel from the shard plan), so the flat
+    buffers are padded to the largest rank's size and no size exchange is needed."""
     flat = torch.cat([f.reshape(-1) for r in runs for f in r.factors]) if runs else torch.zeros(0, device=device)
+    assert flat.numel() == numel[rank], (flat.numel(), numel[rank])
     if world == 1:
         return flat.numel()
-    n = torch.tensor([flat.numel()], device=device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    mx = int(max(s.item() for s in sizes))
-    buf = torch.zeros(mx, device=device)
+    buf = torch.zeros(max(numel), device=device)
     buf[:flat.numel()] = flat
     out = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
     dist.gather(buf, out, dst=0)
-    return sum(int(s.item()) for s in sizes)
+    return sum(numel)
 
 
 def reduce_over_ranks(elapsed, factor_iters, world, device):
@@ -120,34 +133,125 @@ def reduce_over_ranks(elapsed, factor_iters, world, device):
     return float(el.item()), float(fi.item())
 
 
-def algorithmic_flops(work, max_iter_admm, num_attempts=200):
-    """Per step: SSE sweep 8 flops x candidates x elements (SURVEY §8(d) F_valu) and the
-    solve GEMM 2 I R^2, summed over (layer, mode) x inner iterations."""
+PEAK_F16_MFMA = 16 * PEAK_F32  # TFLOP/s dense f16 MFMA (MI355X_MICROARCH.md: 1/16 rate ratio, ~2.5 PF)
+PEAK_HBM = 8.0                 # TB/s HBM3E spec
+THIN_ROWS = 16                 # kThinRows: factors with I <= 16 take k_gemm_thin / k_mse_small_admm
+SPLIT_PRODUCTS = 3             # split-fp16 solve: Ph Mh + Ph Ml + Pl Mh per solve flop
+
+# Launch classes of admmq_profile_end (include/admmq.h ADMMQ_PROF_*) and, per element of
+# an (I, R) factor (or per factor), the algorithmic work one launch does for one
+# problem. Bytes are the compulsory HBM bytes of DESIGN.md §4 (fp32 = 4 B; the split
+# planes are 2 x 2 B = 4 B per element too):
+#   gemm / gemm_thin  H_T = P M: 2 I R^2 flops; read P, U, M, write H_T: 4 (3 I R + R^2) B
+#   search            stage 1 + selection + stage 2 over X = H_T - U: read H_T, U: 8 I R B
+#                     (SURVEY §8(d) counts the reference's exhaustive sweep, 8 x 200 flops
+#                     per element; reported beside the byte roofline as `valu_equiv`)
+#   small             search + finalize of the I <= 16 factors in one block: 8 I R + 28 I R B
+#   finalize          read H_T, H, U, F, write H, U, next P: 28 I R B
+PROF_CLASSES = ["gemm", "gemm_thin", "search", "small", "finalize", "prepare"]
+KERNEL_NAMES = {"gemm": "k_gemm (solve, split-f16 MFMA)", "gemm_thin": "k_gemm_thin (solve, I<=16, VALU)",
+                "search": "k_mse_hist3 (two-stage MSE search)", "small": "k_mse_small_admm (I<=16 search+finalize)",
+                "finalize": "k_finalize_admm (projection + dual update)", "prepare": "prepare (rho, SPD inverse, planes)"}
+
+
+def mode_problems(work):
+    """[(I, R) of every factor solved in mode m] per mode m (bench batches one mode of
+    every layer per admm_iteration_batched call, like admmq.factorize.als_sweep)."""
+    nm = max(len(s.shape) for (s, _, _, _) in work)
+    return [[(s.shape[m], R) for (s, _, R, _) in work if m < len(s.shape)] for m in range(nm)]
+
+
+def class_work(work, num_attempts=200, split=True):
+    """Per launch class: (flops, bytes, valu_equiv_flops) of ONE launch, averaged over the
+    modes whose calls issue it. The HIP-event sampling times one iteration in N of every
+    mode call, so each issuing mode weighs equally in the measured average duration."""
+    out = {}
+    for cls in PROF_CLASSES[:5]:
+        per_mode = []
+        for probs in mode_problems(work):
+            big = [(i, r) for (i, r) in probs if i > THIN_ROWS]
+            thin = [(i, r) for (i, r) in probs if i <= THIN_ROWS]
+            sel = thin if cls in ("gemm_thin", "small") else big
+            if not sel:
+                continue
+            fl = sum(2.0 * i * r * r for (i, r) in sel) if cls.startswith("gemm") else 0.0
+            if cls.startswith("gemm"):
+                by = sum(4.0 * (3 * i * r + r * r) for (i, r) in sel)
+            elif cls == "search":
+                by = sum(8.0 * i * r for (i, r) in sel)
+            elif cls == "small":
+                by = sum(36.0 * i * r for (i, r) in sel)
+            else:
+                by = sum(28.0 * i * r for (i, r) in sel)
+            ve = sum(8.0 * num_attempts * i * r for (i, r) in sel) if cls in ("search", "small") else 0.0
+            per_mode.append((fl, by, ve))
+        if per_mode:
+            n = len(per_mode)
+            out[cls] = tuple(sum(x[k] for x in per_mode) / n for k in range(3))
+    return out
+
+
+def kernel_roofline(cls, work_tuple, avg_us, launches, split, traffic):
+    """Roofline of one launch class: bound = the larger of its MFMA and HBM times at peak
+    (solve: f16 MFMA / 3 products when split, fp32 MFMA otherwise); achieved = algorithmic
+    work per launch / measured average launch duration."""
+    fl, by, ve = work_tuple
+    t = avg_us * 1e-6
+    mf_peak = (PEAK_F16_MFMA / SPLIT_PRODUCTS) if (split and cls == "gemm") else PEAK_F32
+    t_mfma = fl / (mf_peak * 1e12) if fl else 0.0
+    t_hbm = by / (PEAK_HBM * 1e12)
+    if t_mfma > t_hbm:
+        r = {"bound": "mfma", "achieved": fl / t / 1e12, "peak": mf_peak, "unit": "TFLOP/s"}
+    else:
+        r = {"bound": "hbm", "achieved": by / t / 1e9, "peak": PEAK_HBM * 1e3, "unit": "GB/s"}
+    r["frac"] = r["achieved"] / r["peak"]
+    tr = (traffic or {}).get("classes", {}).get(cls)
+    r["traffic"] = tr["bytes_per_launch"] if tr else None
+    r.update({"traffic_unit": "HBM bytes/launch (PMC: 2 FETCH_SIZE + WRITE_SIZE)", "kernel": KERNEL_NAMES[cls],
+              "launch_avg_us": avg_us, "launches_timed": launches, "algorithmic_bytes_per_launch": by,
+              "algorithmic_flops_per_launch": fl, "t_ideal_us": max(t_mfma, t_hbm) * 1e6})
+    if cls == "gemm":
+        r["mfma_form"] = "split-f16 (v_mfma_f32_32x32x16_f16, 3 products)" if split else "fp32 (v_mfma_f32_32x32x2_f32)"
+    if ve:
+        r["valu_equiv"] = {"achieved": ve / t / 1e12, "peak": PEAK_F32, "unit": "TFLOP/s",
+                           "frac": ve / t / 1e12 / PEAK_F32,
+                           "note": "SURVEY §8(d) F_valu: the reference's 200-candidate sweep, 8 flops/candidate-element"}
+    if traffic:
+        r["traffic_source"] = traffic["file"]
+    return r
+
+
+def step_roofline(work, max_iter_admm, ms_per_step, num_attempts=200):
+    """T_ideal = max(F_mfma / 157.3 TF/s, F_valu / 157.3 TF/s, B_hbm / 8 TB/s)
+    per factor-iteration, summed over every (layer, mode) x inner iteration of the step."""
     it = max_iter_admm - 1
-    sse = sum(8.0 * num_attempts * d * R for (s, W, R, _) in work for d in s.shape) * it
-    gemm = sum(2.0 * d * R * R for (s, W, R, _) in work for d in s.shape) * it
-    return sse, gemm
+    f_mfma = sum(2.0 * I * R * R for probs in mode_problems(work) for (I, R) in probs) * it
+    f_valu = sum((8.0 * num_attempts + 20.0) * I * R for probs in mode_problems(work) for (I, R) in probs) * it
+    b_hbm = sum(4.0 * (6 * I * R + R * R) for probs in mode_problems(work) for (I, R) in probs) * it
+    terms = {"mfma_fp32": f_mfma / (PEAK_F32 * 1e12), "valu": f_valu / (PEAK_F32 * 1e12), "hbm": b_hbm / (PEAK_HBM * 1e12)}
+    t_ideal = max(terms.values())
+    return {"t_ideal_ms": t_ideal * 1e3, "t_measured_ms": ms_per_step, "frac": t_ideal * 1e3 / ms_per_step,
+            "terms_ms": {k: v * 1e3 for k, v in terms.items()}, "binding": max(terms, key=terms.get),
+            "formula": "SURVEY §8(d): max(F_mfma/157.3 TF/s, F_valu/157.3 TF/s, B_hbm/8 TB/s) per step"}
 
 
-def gemm_bytes(work):
-    """Algorithmic HBM bytes of the solve GEMMs of one ADMM iteration over every mode:
-    P and U read, H_T and X = H_T - U written (4 I R floats) and M read (R^2 floats)."""
-    return sum(4.0 * (4 * d * R + R * R) for (s, W, R, _) in work for d in s.shape)
+TRAFFIC_TAG = "r02"
 
 
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_v9_traffic.json")
-
-
-def load_traffic():
-    """Per-launch HBM bytes of each launch class from the committed rocprofv3 PMC passes
-    (tools/traffic_json.py); PMC counters cannot be read live inside the timed region."""
+def load_traffic(model, split):
+    """Per-launch HBM bytes of each launch class from the committed rocprofv3 PMC passes of
+    THIS config (profiles/<tag>_<model>_traffic.json, tools/traffic_json.py); PMC counters
+    cannot be read live inside the timed region. None when no file matches the config."""
+    path = os.path.join(ROOT, "profiles", f"{TRAFFIC_TAG}_{model}_traffic.json")
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(path) as f:
             t = json.load(f)
-        t["file"] = os.path.relpath(TRAFFIC_FILE, os.path.dirname(os.path.abspath(__file__)))
-        return t
     except (OSError, ValueError):
         return None
+    if t.get("split", True) != split:
+        return None
+    t["file"] = os.path.relpath(path, ROOT)
+    return t
 
 
 def cpu_baseline(work, max_iter_admm, sample_iters=20):
@@ -211,13 +315,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--max-iter-admm", type=int, default=1000)
-    ap.add_argument("--shard", choices=["replica", "layers"], default="replica")
+    ap.add_argument("--shard", choices=["layers", "replica"], default="layers",
+                    help="layers: LPT-shard one model's layers over the ranks (default); replica: every rank its own copy")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-iters", type=int, default=None,
                     help="inner iterations timed per (layer, mode) on the CPU (default 20; 1 for llama7b)")
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP-event timing of one ADMM iteration in N (an event pair per launch adds a gap)")
+    ap.add_argument("--solve", choices=["split", "fp32"], default="split",
+                    help="per-iteration solve GEMM form: split-fp16 planes on f16 MFMA (default) or fp32 MFMA")
     ap.add_argument("--exhaustive", action="store_true",
                     help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
     a = ap.parse_args()
@@ -233,16 +340,18 @@ def main():
     from admmq import _lib
     lib = _lib.load()
     lib.admmq_set_exhaustive_search(1 if a.exhaustive else 0)
-    work = build_workload(a.model, rank, world, a.shard, device)
+    _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
+    split = a.solve == "split"
+    work, numel, shard_info = build_workload(a.model, rank, world, a.shard, device)
     fi_per_step = sum(len(s.shape) * (a.max_iter_admm - 1) for (s, _, _, _) in work)
 
     for _ in range(a.warmup):
-        gather_factors(run_step(work, a.max_iter_admm), rank, world, device)
+        gather_factors(run_step(work, a.max_iter_admm), rank, world, numel, device)
     torch.cuda.synchronize()
 
     prof = not a.no_profile
     if prof:
-        n_launch = a.steps * 3 * 3 * (a.max_iter_admm // a.prof_every + 1) + 64
+        n_launch = a.steps * 3 * 6 * (a.max_iter_admm // a.prof_every + 1) + 64
         _lib.check(lib.admmq_profile_begin(n_launch, a.prof_every), "profile_begin")
     if world > 1:
         dist.barrier()
@@ -250,7 +359,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         runs = run_step(work, a.max_iter_admm)
-        gather_factors(runs, rank, world, device)
+        gather_factors(runs, rank, world, numel, device)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -258,8 +367,8 @@ def main():
     kern = None
     if prof:
         import ctypes
-        ms = (ctypes.c_double * 4)()
-        cnt = (ctypes.c_int64 * 4)()
+        ms = (ctypes.c_double * 8)()
+        cnt = (ctypes.c_int64 * 8)()
         _lib.check(lib.admmq_profile_end(ms, cnt), "profile_end")
         kern = {"ms": list(ms), "launches": list(cnt)}
 
@@ -269,43 +378,36 @@ def main():
         out = {"metric": METRIC, "value": total_fi / elapsed_max, "unit": "factor-iterations/s", "n_gpus": world,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * elapsed_max / a.steps,
                "higher_is_better": True, "scaling": "weak" if a.shard == "replica" else "strong",
-               "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+               "vs_baseline": None,
+               "dtype": "f32 (solve: split-f16 MFMA, fp32 accumulate)" if split else "f32", "data": "synthetic",
                "config": {"workload": workload_name(a.model, work, a.max_iter_admm),
                           "factor_iterations_per_step_per_gpu": fi_per_step, "max_iter_admm": a.max_iter_admm,
                           "parallelism": f"{'replica' if a.shard == 'replica' else 'layer-shard'} x{world}, "
                                          "one RCCL gather of factors per step",
-                          "mse_search": "exhaustive" if a.exhaustive else "two-stage exact"}}
+                          "mse_search": "exhaustive" if a.exhaustive else "two-stage exact",
+                          "solve": a.solve}}
+        out["step_roofline"] = step_roofline(work, a.max_iter_admm, out["ms_per_step"])
+        if shard_info:
+            out["config"]["shard"] = shard_info
         if kern is not None:
-            sse_f, gemm_f = algorithmic_flops(work, a.max_iter_admm)
             ms, cnt = kern["ms"], kern["launches"]
-            # one ADMM iteration in prof_every is timed, uniformly over the modes, so the
-            # class's average launch duration is ms/cnt and its average algorithmic flops
-            # per launch is the step's total over all the step's launches
-            n_modes = max(len(s.shape) for (s, _, _, _) in work)
-            launches_per_step = n_modes * (a.max_iter_admm - 1)
-            avg_us = [1e3 * ms[i] / max(cnt[i], 1) for i in range(4)]
-            traffic = load_traffic()
-            rf = []
-            for cls, (flops, bound, name) in enumerate([
-                    (gemm_f, "mfma", "k_gemm (solve, MFMA f32)"),
-                    (sse_f, "valu", "MSE search (k_mse_hist3: stage 1 + selection + stage 2)")]):
-                ach = flops / launches_per_step / (avg_us[cls] * 1e-6) / 1e12 if cnt[cls] else 0.0
-                key = ["gemm", "sse"][cls]
-                r = {"bound": bound, "achieved": ach, "peak": PEAK_F32, "unit": "TFLOP/s", "frac": ach / PEAK_F32,
-                     "traffic": traffic["classes"][key]["bytes_per_launch"] if traffic else None,
-                     "traffic_unit": "bytes/launch (HBM, PMC)", "kernel": name,
-                     "launch_avg_us": avg_us[cls], "launches_timed": cnt[cls]}
-                if traffic:
-                    r["traffic_source"] = traffic["file"]
-                if cls == 0:
-                    r["algorithmic_bytes_per_launch"] = gemm_bytes(work) / n_modes
-                rf.append(r)
-            dom = max(range(3), key=lambda k: avg_us[k])
-            out["roofline"] = rf[1] if dom == 1 else rf[0]
-            out["roofline_gemm"] = rf[0]
-            out["kernel_ms_per_step"] = {k: avg_us[i] * 1e-3 * (launches_per_step if i < 3 else cnt[3] / a.steps)
-                                         for i, k in enumerate(["gemm", "sse", "finalize", "prepare"])}
-            out["kernel_avg_us"] = dict(zip(["gemm", "sse", "finalize", "prepare"], avg_us))
+            avg_us = {c: 1e3 * ms[i] / cnt[i] for i, c in enumerate(PROF_CLASSES) if cnt[i]}
+            traffic = load_traffic(a.model, split)
+            cw = class_work(work, split=split)
+            rf = {c: kernel_roofline(c, cw[c], avg_us[c], cnt[i], split, traffic)
+                  for i, c in enumerate(PROF_CLASSES[:5]) if c in cw and c in avg_us}
+            # per step: each class launches once per inner iteration of every mode that issues it
+            n_issuing = {c: sum(1 for probs in mode_problems(work)
+                                if any((i <= THIN_ROWS) == (c in ("gemm_thin", "small")) for (i, _) in probs))
+                         for c in PROF_CLASSES[:5]}
+            per_step = {c: avg_us[c] * 1e-3 * n_issuing[c] * (a.max_iter_admm - 1) for c in rf}
+            if "prepare" in avg_us:
+                per_step["prepare"] = avg_us["prepare"] * 1e-3 * cnt[PROF_CLASSES.index("prepare")] / a.steps
+            dom = max(rf, key=lambda c: per_step[c])
+            out["roofline"] = rf[dom]
+            out["roofline_kernels"] = rf
+            out["kernel_ms_per_step"] = per_step
+            out["kernel_avg_us"] = avg_us
             out["prof_every"] = a.prof_every
         if world == 1 and not a.no_cpu_baseline:
             # cpu_baseline leg: the CPU reference port timed on host cores, and the

@@ -114,12 +114,24 @@ int32_t admmq_set_exhaustive_search(int32_t enable);
 int32_t admmq_set_solve_mode(int32_t mode);
 int32_t admmq_get_solve_mode(void);
 
-/* Optional HIP-event timing of every launch class issued by admmq_admm_prepare/run on
- * this thread between begin and end: class 0 GEMM (solve), 1 MSE candidate sweep,
- * 2 projection/dual update, 3 whole prepare phase. Only ADMM iterations it with
+/* Optional HIP-event timing of every launch issued by admmq_admm_prepare/run on this
+ * thread between begin and end, one event pair per launch, summed per class:
+ * ADMMQ_PROF_GEMM k_gemm (solve, MFMA), ADMMQ_PROF_GEMM_THIN k_gemm_thin (solve of the
+ * I <= 16 factors, VALU), ADMMQ_PROF_SEARCH the multi-block MSE candidate search
+ * (k_mse_hist3 / k_mse_hist / the exhaustive sweep), ADMMQ_PROF_SMALL k_mse_small_admm
+ * (search + projection + dual update of the I <= 16 factors in one block each),
+ * ADMMQ_PROF_FINALIZE k_finalize_admm (projection + dual update), ADMMQ_PROF_PREPARE the
+ * whole prepare phase (rho, SPD inverse, operand planes). Only ADMM iterations it with
  * it % sample_every == 0 are timed (each event pair adds an inter-kernel gap, so the
  * bench samples instead of timing every launch). end() synchronises on the last event
- * and returns summed milliseconds and launch counts per class (arrays of 4). */
+ * and fills ADMMQ_PROF_CLASSES summed milliseconds and launch counts. */
+#define ADMMQ_PROF_GEMM 0
+#define ADMMQ_PROF_GEMM_THIN 1
+#define ADMMQ_PROF_SEARCH 2
+#define ADMMQ_PROF_SMALL 3
+#define ADMMQ_PROF_FINALIZE 4
+#define ADMMQ_PROF_PREPARE 5
+#define ADMMQ_PROF_CLASSES 8
 int32_t admmq_profile_begin(int32_t max_launches, int32_t sample_every);
 int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class);
 

@@ -36,16 +36,17 @@ def _worker(rank, port, shard, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
         dev = torch.device("cpu")
-        work = bench.build_workload("resnet18", rank, WORLD, shard, dev)
+        work, numel, info = bench.build_workload("resnet18", rank, WORLD, shard, dev)
         names = [s.name for (s, _, _, _) in work]
         wsum = float(sum(W.double().sum() for (_, W, _, _) in work))
         runs = [LayerRun(s.name, W, R, [f.clone() for f in init]) for (s, W, R, init) in work]
         n_local = sum(f.numel() for r in runs for f in r.factors)
-        gathered = bench.gather_factors(runs, rank, WORLD, dev)
+        assert numel[rank] == n_local   # the static shard plan knows every rank's size
+        gathered = bench.gather_factors(runs, rank, WORLD, numel, dev)
         el, fi = bench.reduce_over_ranks(1.0 + rank, 100 * (rank + 1), WORLD, dev)
         specs = synthetic.MODELS["resnet18"]()
         dist.destroy_process_group()
-        q.put((rank, names, wsum, n_local, gathered, el, fi, len(specs)))
+        q.put((rank, names, wsum, n_local, gathered, el, fi, len(specs), info))
     except Exception as e:  # surfaced by the parent
         q.put((rank, "error", repr(e)))
 
@@ -90,6 +91,11 @@ def test_layer_sharding_partitions_model():
     assert set(r0[1]).isdisjoint(r1[1])
     assert len(r0[1]) + len(r1[1]) == r0[7]
     assert r0[4] == r1[4] == r0[3] + r1[3]
+    # the line's LPT cap: total cost over the busiest rank's, <= world and <= the whole-layer cap
+    info = r0[8]
+    assert info["layers_per_rank"] == [len(r0[1]), len(r1[1])]
+    assert 1.0 < info["lpt_speedup_cap"] <= WORLD
+    assert info["whole_layer_speedup_cap"] == pytest.approx(4.2, abs=0.1)   # resnet18
 
 
 def test_lpt_balance():

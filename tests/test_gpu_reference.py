@@ -11,7 +11,12 @@
               step-1 flip every difference is a near-half rounding of step 2 (the
               reference itself is chaotic at the 1-ulp level); with no level
               difference, H within 1e-4 rel-Frob;
-    it6:      at most 0.5 % of the levels differ and the scale agrees to 1e-5.
+    it6:      the result lies ON one of the reference's own branches (F8,
+              tests/golden/gen_f8_branches.py: the reference re-run with its
+              cholesky_solve moved by <= 1 ulp per element reaches, e.g. for
+              tensor_symmetric mode 0, two trajectories with scales 10.8 % apart):
+              scale within 1e-5 of a branch's and at most 0.5 % of the levels
+              differing from that branch's H. F2 stores one sample of them.
   tensor_minmax has no uniform grid (source/quantization.py:48-66): H within 1e-5.
 * F7 (tests/golden/f7_neartie.*): quantizer inputs captured from the reference's own
   ADMM at steps 5, 50, 500 (tests/golden/gen_f7.py). The HIP quantizer output must
@@ -98,8 +103,24 @@ def test_f2_reference_horizons(torch_dev, mode, qscheme, solve):
             if n_bad == 0:
                 assert _rel(H, rH) < 1e-4, report
         else:
-            assert srel < 1e-5 and n_bad <= 5e-3 * H.size, report
+            bH, frac = _reference_branch(mode, qscheme, s)
+            assert bH is not None, (report, "it6 scale on no reference branch", float(s))
+            n_bad, _ = gc.level_mismatch(H, bH, X)
+            report[mi].update(branch_frequency=frac, branch_mismatches=n_bad)
+            assert n_bad <= 5e-3 * H.size, report
     print(mode, qscheme, solve, report)
+
+
+def _reference_branch(mode, qscheme, scale):
+    """(H, frequency) of the F8 reference branch whose scale is within 1e-5 of `scale`."""
+    with open(os.path.join(GOLDEN, "f8_branches.json")) as f:
+        meta = {c["key"]: c for c in json.load(f)["cases"]}
+    c = meta[f"m{mode}_{qscheme}"]
+    z = np.load(os.path.join(GOLDEN, "f8_branches.npz"))
+    for j, b in enumerate(c["branches"]):
+        if abs(float(scale) - b["scale"]) / b["scale"] < 1e-5:
+            return z[f"{c['key']}_b{j}_H"], b["count"] / c["trials"]
+    return None, 0.0
 
 
 def test_f2_two_way_reference(torch_dev):

@@ -76,3 +76,22 @@ def test_sse_table_is_order_independent():
     xp = x[::-1].copy()
     sse2, _, _ = qo.mse_sse_table(xp, 4)
     assert np.array_equal(sse, sse2)
+
+
+def test_f8_reference_branches_pin_f2_and_oracle():
+    """F8 (the reference re-run with <= 1-ulp solve perturbations): its most frequent
+    branch is F2's stored it6 sample, and the oracle's own 5-step run lies on a branch."""
+    from oracle import admm_oracle as ao
+    z2 = np.load(os.path.join(GOLDEN, "f2_admm.npz"))
+    z8 = np.load(os.path.join(GOLDEN, "f8_branches.npz"))
+    with open(os.path.join(GOLDEN, "f8_branches.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == 5
+    for c in cases:
+        mode, qs = c["mode"], c["qscheme"]
+        assert sum(b["count"] for b in c["branches"]) <= c["trials"]
+        assert np.array_equal(z8[f"{c['key']}_b0_H"], z2[f"l1_m{mode}_{qs}_it6_H"]), c["key"]
+        G, F, H0 = z2[f"l1_m{mode}_G"], z2[f"l1_m{mode}_F"], z2["l1_" + "ABC"[mode]]
+        H, _ = ao.admm_iteration(H0, np.zeros_like(H0), F, G, 6, 1e-8, 4, qs)
+        _, s = gc.grid_levels(H)
+        assert any(abs(float(s) - b["scale"]) / b["scale"] < 1e-5 for b in c["branches"]), (c["key"], float(s))

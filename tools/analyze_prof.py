@@ -36,13 +36,18 @@ def main(d, tag, out):
     fetch, fcalls = read_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
     write, wcalls = read_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
     sq, scalls = read_counters(os.path.join(d, "pmc_sq", "run_counter_collection.csv"))
+    tcc, tcalls = read_counters(os.path.join(d, "pmc_tcc", "run_counter_collection.csv"))
     lines = [f"# rocprofv3 summary `{tag}`", "",
-             "Kernel-trace stats of `python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile` "
-             "(C3 workload). PMC columns come from separate passes on a 20-iteration schedule "
+             "Kernel-trace stats of `python3 bench.py --model <model> --steps 2 --warmup 1 --no-cpu-baseline --no-profile` "
+             f"(directory `{d}`). PMC columns come from separate passes on a 20-iteration schedule "
              "(`--max-iter-admm 21`), per launch. FETCH bytes are FETCH_SIZE x 1024 x 2 (gfx950 correction), "
              "WRITE bytes WRITE_SIZE x 1024.", "",
-             "| kernel | calls | avg us | share % | FETCH MB/launch (x2 corr.) | WRITE MB/launch | VALU instr/launch | MFMA instr/launch |",
-             "|---|---|---|---|---|---|---|---|"]
+             "MFMA busy % = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) (GRBM_GUI_ACTIVE sums the 8 XCDs; "
+             "MI355X_MICROARCH.md). LDS conflicts are SQ_LDS_BANK_CONFLICT extra cycles per LDS instruction. "
+             "L2 hit % = TCC_HIT / (TCC_HIT + TCC_MISS).", "",
+             "| kernel | calls | avg us | share % | FETCH MB/launch (x2 corr.) | WRITE MB/launch | VALU instr/launch | "
+             "MFMA instr/launch | MFMA busy % | LDS confl./instr | L2 hit % |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows[:25]:
         k = short(r["Name"])
         nf = max(len(fcalls.get(k, ())), 1)
@@ -52,8 +57,17 @@ def main(d, tag, out):
         wb = write[k].get("WRITE_SIZE", 0.0) * 1024 / nw / 1e6 if k in write else float("nan")
         va = sq[k].get("SQ_INSTS_VALU", float("nan")) / ns if k in sq else float("nan")
         mf = sq[k].get("SQ_INSTS_MFMA", float("nan")) / ns if k in sq else float("nan")
+        nan = float("nan")
+        busy = nan
+        if k in sq and sq[k].get("GRBM_GUI_ACTIVE"):
+            busy = 100.0 * sq[k].get("SQ_VALU_MFMA_BUSY_CYCLES", nan) / (sq[k]["GRBM_GUI_ACTIVE"] / 8 * 1024)
+        confl = sq[k].get("SQ_LDS_BANK_CONFLICT", nan) / sq[k]["SQ_INSTS_LDS"] if k in sq and sq[k].get("SQ_INSTS_LDS") else nan
+        hit = nan
+        if k in tcc:
+            h, m = tcc[k].get("TCC_HIT_sum", 0.0), tcc[k].get("TCC_MISS_sum", 0.0)
+            hit = 100.0 * h / (h + m) if h + m else nan
         lines.append(f"| `{k}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} | "
-                     f"{fb:.2f} | {wb:.2f} | {va:.3g} | {mf:.3g} |")
+                     f"{fb:.2f} | {wb:.2f} | {va:.3g} | {mf:.3g} | {busy:.1f} | {confl:.2f} | {hit:.1f} |")
     open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 

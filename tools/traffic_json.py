@@ -7,7 +7,8 @@ like bench.py's sampled HIP-event timing). FETCH_SIZE is doubled: on gfx950 it r
 half the bytes of a wide coalesced stream (MI355X_MICROARCH.md, HBM section); FETCH
 and WRITE come from separate passes. Writes profiles/<tag>_traffic.json, which bench.py
 reads into roofline.traffic.
-usage: tools/traffic_json.py gpurun_out/prof_<tag> <tag>
+usage: tools/traffic_json.py gpurun_out/prof_<tag> <tag> [model] [split|fp32]
+(writes profiles/<tag>_<model>_traffic.json)
 """
 import csv
 import json
@@ -15,7 +16,9 @@ import os
 import sys
 from collections import defaultdict
 
-CLASSES = {"gemm": ("k_gemm",), "sse": ("k_mse_",), "finalize": ("k_finalize_admm",)}
+# bench.py's launch classes (ADMMQ_PROF_*) by kernel-name prefix
+CLASSES = {"gemm": ("k_gemm<",), "gemm_thin": ("k_gemm_thin",), "search": ("k_mse_hist", "k_mse_sse", "k_mse_select"),
+           "small": ("k_mse_small_admm",), "finalize": ("k_finalize_admm",)}
 
 
 def per_dispatch(path, counter):
@@ -33,11 +36,13 @@ def per_dispatch(path, counter):
 
 def main():
     d, tag = sys.argv[1], sys.argv[2]
+    model = sys.argv[3] if len(sys.argv) > 3 else "resnet18"
+    solve = sys.argv[4] if len(sys.argv) > 4 else "split"
     fetch, fn = per_dispatch(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write, wn = per_dispatch(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     res = {"source": f"gpurun_out/prof_{tag} (tools/profile.sh), summarised in profiles/{tag}_summary.md",
            "formula": "2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH correction), separate PMC passes",
-           "classes": {}}
+           "model": model, "split": solve == "split", "classes": {}}
     for cls, pref in CLASSES.items():
         fv = [v for k, v in fetch.items() if fn[k].startswith(pref)]
         wv = [v for k, v in write.items() if wn[k].startswith(pref)]
@@ -47,7 +52,7 @@ def main():
         res["classes"][cls] = {"fetch_bytes": 2 * f_avg, "write_bytes": w_avg, "bytes_per_launch": 2 * f_avg + w_avg,
                                "launches": [len(fv), len(wv)]}
     os.makedirs("profiles", exist_ok=True)
-    with open(os.path.join("profiles", f"{tag}_traffic.json"), "w") as f:
+    with open(os.path.join("profiles", f"{tag}_{model}_traffic.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
 

@@ -112,6 +112,13 @@ struct GemmTile {
   const int* eP; const int* eM;
   int ld, ldm;
 };
+// Stream-K piece of the wide split solve (k_gemm_sk): K-steps [k0, k1) of tile `tile`
+// (a GemmTile of 128 x 128). A tile cut over np > 1 pieces has partial slots
+// part .. part + np - 1 (this piece: part + pidx) and arrival counter `cnt`; the last of
+// its pieces to arrive sums the partials in pidx order and runs the epilogue. `first`:
+// the piece owns the problem's per-iteration duties (sticky stop flag, zeroing the
+// search accumulators) - the k0 == 0 piece of tile (0, 0).
+struct SkPiece { int tile, k0, k1, np, pidx, part, cnt, first; };
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
 struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
 // Work unit {job, first element}. Stage-1 units also carry the job's inputs that the
@@ -177,6 +184,8 @@ void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int 
                       int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
                  int iter, float eps, int ncand, hipStream_t s);
+void launch_gemm_sk(const ProbDesc* d, const GemmTile* tiles, const SkPiece* pieces, const int2* ranges, int nwg,
+                    float* part, unsigned* cnt, int slot, int iter, float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,

@@ -13,7 +13,9 @@ from typing import Sequence
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libadmmq.so")
+# ADMMQ_LIB: another build of the same library (diagnostics only, e.g. the TRACE=1
+# build libadmmq_trace.so read by tools/*_timeline.py)
+LIB_PATH = os.environ.get("ADMMQ_LIB") or os.path.join(_HERE, "libadmmq.so")
 
 SCHEMES = {
     "tensor_mseminmax_symmetric": 0,
@@ -67,6 +69,8 @@ def load() -> ctypes.CDLL:
         "admmq_get_solve_mode": (I32, []),
         "admmq_debug_set_legacy_stage1": (I32, [I32]),
         "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
+        "admmq_debug_check_thresholds": (I32, [ctypes.c_uint32, I32]),
+        "admmq_debug_check_cells": (I32, [I32, I32, ctypes.c_uint32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
         "admmq_profile_end": (I32, [P, P]),
         "admmq_cp_workspace_size": (S, [P, I32, I32]),

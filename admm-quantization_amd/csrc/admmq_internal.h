@@ -33,6 +33,7 @@ constexpr int kMaxStage1 = 1024;   // num_attempts handled by the two-stage sear
 constexpr int kMaxStage1Bits = 6;  // bits handled by the two-stage search (threshold table in LDS)
 constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms (atomic spread)
 constexpr int kMaxMerged = 4096;   // qmax * ncand of the merged-threshold stage 1
+constexpr int kCells = 4096;       // coarse cells of the merged-threshold stage 1 (mse_search.hip)
 constexpr int kResRep = 8;         // replicas of the per-problem residual sums (atomic spread)
 constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU split-K solve
 constexpr int kThinCols = 256;     // ... columns per unit (64 lanes x float4)
@@ -112,13 +113,6 @@ struct GemmTile {
   const int* eP; const int* eM;
   int ld, ldm;
 };
-// Stream-K piece of the wide split solve (k_gemm_sk): K-steps [k0, k1) of tile `tile`
-// (a GemmTile of 128 x 128). A tile cut over np > 1 pieces has partial slots
-// part .. part + np - 1 (this piece: part + pidx) and arrival counter `cnt`; the last of
-// its pieces to arrive sums the partials in pidx order and runs the epilogue. `first`:
-// the piece owns the problem's per-iteration duties (sticky stop flag, zeroing the
-// search accumulators) - the k0 == 0 piece of tile (0, 0).
-struct SkPiece { int tile, k0, k1, np, pidx, part, cnt, first; };
 // Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
 struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
 // Work unit {job, first element}. Stage-1 units also carry the job's inputs that the
@@ -133,6 +127,7 @@ struct Chunk {
   long long total;
   const float* H;   // ADMM finalize units: the current H and the padded F
   const float* F;
+  const int* sel;   // ADMM finalize units: the job's search record [slot][2 + kMaxSel]
 };
 
 // Loads through global (not flat) pointers: flat loads also count in lgkmcnt, and a
@@ -184,8 +179,6 @@ void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int 
                       int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
                  int iter, float eps, int ncand, hipStream_t s);
-void launch_gemm_sk(const ProbDesc* d, const GemmTile* tiles, const SkPiece* pieces, const int2* ranges, int nwg,
-                    float* part, unsigned* cnt, int slot, int iter, float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
@@ -197,6 +190,7 @@ int copy_setup_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
 int check_thresholds(unsigned seed, int nsamp);
+int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out);
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s);

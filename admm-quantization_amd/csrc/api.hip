@@ -74,13 +74,19 @@ static bool two_stage_ok(int ncand, int bits) {
 // the order; rank0[e] for e = (k-1) n + c, and the groups of equal keys as
 // {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
 // than 4 (the per-level stage 1 is used instead).
+// rank0 is returned padded to kMaxMerged entries and followed by the coarse cell index
+// lower bound lo[g], g = 0..kCells (see h3_setup): the number of thresholds whose cell
+// (floor of threshold * kCells / largest threshold) is below g for EVERY mx. A
+// threshold's cell is floor(z (1 + d)) with z = kCells key / key_max and |d| a few ulps
+// (the float thresholds and the cell scale each within ~10 ulps of the key proportion),
+// so counting the keys with z (1 + 1e-4) < g can only undercount.
 static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, std::vector<unsigned short>& groups) {
   const int M = qmax * n;
   std::vector<std::pair<long long, int>> key(M);
   for (int k = 1; k <= qmax; ++k)
     for (int c = 0; c < n; ++c) key[(k - 1) * n + c] = {(long long)(2 * k - 1) * ((n - 1) + 5LL * c), (k - 1) * n + c};
   std::sort(key.begin(), key.end());
-  rank0.assign(M, 0);
+  rank0.assign(kMaxMerged + kCells + 2, 0);
   groups.clear();
   for (int r = 0; r < M;) {
     int r1 = r + 1;
@@ -93,6 +99,12 @@ static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, s
       groups.insert(groups.end(), g, g + 6);
     }
     r = r1;
+  }
+  const double kmax = (double)key[M - 1].first;
+  int cnt = 0;
+  for (int g = 0; g <= kCells; ++g) {
+    while (cnt < M && (double)kCells * (double)key[cnt].first / kmax * (1.0 + 1e-4) < (double)g) ++cnt;
+    rank0[kMaxMerged + g] = (unsigned short)cnt;
   }
   return true;
 }
@@ -141,21 +153,11 @@ struct AdmmPlan {
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
   bool split = false;            // per-iteration solve on the split fp16 planes (kSolveSplit)
-  // stream-K wide split solve (k_gemm_sk): 128 x 128 tiles, pieces, per-workgroup ranges
-  std::vector<GemmTile> sk_tiles;
-  std::vector<SkPiece> sk_pieces;
-  std::vector<int2> sk_ranges;
-  GemmTile* d_sk_tiles = nullptr;
-  SkPiece* d_sk_pieces = nullptr;
-  int2* d_sk_ranges = nullptr;
-  float* d_sk_part = nullptr;      // [nslabs][128 x 128] partial tiles
-  unsigned* d_sk_cnt = nullptr;    // [nskcnt] arrival counters of the cut tiles (zeroed per run)
-  int sk_nwg = 0, sk_nslabs = 0, sk_ncnt = 0;
   std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
   ThinUnit* d_thin = nullptr;
   unsigned* d_tcnt = nullptr;    // their per-column-block arrival counters
   int thin_nr = 0, ntcnt = 0;
-  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged)
+  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged), then the cell index (kCells + 2)
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
@@ -217,57 +219,6 @@ static int fin_groups_for(const std::vector<ProbDesc>& desc, const std::vector<i
   return g;
 }
 
-// Stream-K decomposition of the wide split solve (k_gemm_sk). Tiles are 128 x 128,
-// per problem column-panel-major (the row tiles of one M column panel adjacent). Their
-// K-steps, in tile order, form one sequence of S steps, cut into nwg ranges of T steps
-// (T = ceil(S / 256), at least kSkMinSteps so that small problem sets are not shredded
-// into partial tiles); nwg is rounded up to a multiple of 8 (the XCD mapping of
-// k_gemm_sk; trailing ranges are empty). A tile crossing a range boundary becomes np
-// pieces with np partial slabs and one arrival counter.
-static constexpr int kSkMinSteps = 4;
-static void plan_stream_k(AdmmPlan& pl) {
-  pl.sk_tiles.clear(); pl.sk_pieces.clear(); pl.sk_ranges.clear();
-  pl.sk_nwg = pl.sk_nslabs = pl.sk_ncnt = 0;
-  long long S = 0;
-  for (int i = 0; i < (int)pl.desc.size(); ++i) {
-    const ProbDesc& d = pl.desc[i];
-    if (d.I <= kThinRows) continue;
-    const int TM = (d.Ip + 127) / 128, TN = (d.ld + 127) / 128;
-    for (int tn = 0; tn < TN; ++tn)
-      for (int tm = 0; tm < TM; ++tm) {
-        pl.sk_tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
-        S += d.ld / 32;
-      }
-  }
-  if (S == 0) return;
-  const long long T = std::max<long long>(kSkMinSteps, (S + 255) / 256);
-  const int nwg = (int)((S + T - 1) / T);
-  pl.sk_nwg = (nwg + 7) / 8 * 8;
-  pl.sk_ranges.assign(pl.sk_nwg, int2{0, 0});
-  // pieces, grouped by range in order
-  std::vector<std::vector<SkPiece>> by_wg(pl.sk_nwg);
-  long long off = 0;
-  for (int t = 0; t < (int)pl.sk_tiles.size(); ++t) {
-    const int nk = pl.sk_tiles[t].nk;
-    const long long w0 = off / T, w1 = (off + nk - 1) / T;
-    const int np = (int)(w1 - w0 + 1);
-    const int part = np > 1 ? pl.sk_nslabs : 0, cnt = np > 1 ? pl.sk_ncnt : 0;
-    if (np > 1) { pl.sk_nslabs += np; pl.sk_ncnt += 1; }
-    for (long long w = w0; w <= w1; ++w) {
-      const long long a = std::max(off, w * T), b = std::min(off + nk, (w + 1) * T);
-      SkPiece pc;
-      pc.tile = t; pc.k0 = (int)(a - off); pc.k1 = (int)(b - off); pc.np = np; pc.pidx = (int)(w - w0);
-      pc.part = part; pc.cnt = cnt; pc.first = (pl.sk_tiles[t].first && pc.k0 == 0) ? 1 : 0;
-      by_wg[w].push_back(pc);
-    }
-    off += nk;
-  }
-  for (int w = 0; w < pl.sk_nwg; ++w) {
-    pl.sk_ranges[w] = int2{(int)pl.sk_pieces.size(), (int)by_wg[w].size()};
-    pl.sk_pieces.insert(pl.sk_pieces.end(), by_wg[w].begin(), by_wg[w].end());
-  }
-}
-
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
   if (nprob <= 0 || !probs) return fail(ADMMQ_ERR_ARG, "no problems");
   if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
@@ -320,40 +271,35 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     pl.maxldm = std::max(pl.maxldm, d.ldm); pl.maxnbk = std::max(pl.maxnbk, d.nbk);
     pl.maxI = std::max(pl.maxI, d.I); pl.maxR = std::max(pl.maxR, d.R);
   }
+  // GEMM tiles, longest K first (LPT over the grid); `first` marks tile (0,0).
+  // 64x64 tiles (Ip > 32) first, then the 32x64 tiles of the 17..32-row factors.
+  // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
+  // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
+  // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
+  pl.tiles.clear();
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
-  pl.tiles.clear();
-  pl.ntiles_big = pl.ntiles_small = 0;
-  if (pl.split) {
-    plan_stream_k(pl);
-  } else {
-    // fp32 form (k_gemm): 64x64 tiles (Ip > 32) first, longest K first (LPT over the grid),
-    // then the 32x64 tiles of the 17..32-row factors; `first` marks tile (0,0).
-    // XCD-aware order: workgroups b and b+8 share an XCD (round-robin dispatch), so the
-    // row tiles that read the same B tile (one column tile tn of M) are laid out 8 apart:
-    // within each group of up to 8 column tiles, positions run tm-major, tn-minor.
-    for (int i : order) {
-      const ProbDesc& d = pl.desc[i];
-      if (d.I <= kThinRows || d.Ip == 32) continue;   // thin: k_gemm_thin units below; 32-row tiles after
-      const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
-      for (int g0 = 0; g0 < TN; g0 += 8)
-        for (int tm = 0; tm < TM; ++tm)
-          for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
-            pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
-    }
-    order_tiles_for_cus(pl.tiles, 256, 3);
-    std::vector<GemmTile> small;
-    for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
-      const ProbDesc& d = pl.desc[i];
-      if (d.I <= kThinRows || d.Ip != 32) continue;
-      const int TN = (d.ld + 63) / 64;
-      for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
-    }
-    pl.ntiles_big = (int)pl.tiles.size();
-    pl.ntiles_small = (int)small.size();
-    pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip == 32) continue;   // thin: k_gemm_thin units below; 32-row tiles after
+    const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
+    for (int g0 = 0; g0 < TN; g0 += 8)
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
+          pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
   }
+  order_tiles_for_cus(pl.tiles, 256, 3);
+  std::vector<GemmTile> small;
+  for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip != 32) continue;
+    const int TN = (d.ld + 63) / 64;
+    for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
+  }
+  pl.ntiles_big = (int)pl.tiles.size();
+  pl.ntiles_small = (int)small.size();
+  pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
   // thin units, most reduction blocks first; counters: one per (problem, column block)
   pl.thin.clear();
   pl.ntcnt = 0;
@@ -393,7 +339,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       const long long step = d.ld <= fin_cap ? (fin_cap / d.ld) * d.ld : fin_cap;
       d.fin_rows = d.ld <= fin_cap ? (int)(fin_cap / d.ld) : 0;
       for (long long e = 0; e < tot; e += step)
-        pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + step), d.H, d.Fp});
+        pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + step), d.H, d.Fp, d.mv.sel});
       const long long hu = (long long)kHistElems * pl.hist_nv;
       for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
       d.mv.nhist = (int)((tot + hu - 1) / hu);
@@ -409,16 +355,11 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
-  pl.d_sk_tiles = cv.take<GemmTile>(pl.sk_tiles.size());
-  pl.d_sk_pieces = cv.take<SkPiece>(pl.sk_pieces.size());
-  pl.d_sk_ranges = cv.take<int2>(pl.sk_ranges.size());
-  pl.d_sk_part = cv.take<float>((size_t)pl.sk_nslabs * 128 * 128);
-  pl.d_sk_cnt = cv.take<unsigned>(std::max(pl.sk_ncnt, 1));
   pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
   pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
   for (int i = 0; i < nprob; ++i)
     if (tcnt_off[i] >= 0 && pl.d_tcnt) pl.desc[i].tcnt = pl.d_tcnt + tcnt_off[i];
-  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged);
+  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged + kCells + 2);
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
@@ -438,17 +379,6 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
     }
   }
   if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
-  for (GemmTile& t : pl.sk_tiles) {   // split planes (row strides in floats unchanged); pad_ carries Ip
-    const ProbDesc& d = pl.desc[t.prob];
-    t.U = d.U; t.ld = d.ld; t.ldm = d.ldm; t.pad_ = d.Ip;
-    t.P = reinterpret_cast<const float*>(d.P2); t.M = reinterpret_cast<const float*>(d.M2);
-    t.eP = d.eP; t.eM = d.eM;
-  }
-  if (!pl.sk_tiles.empty()) {
-    if ((rc = h2d(pl.d_sk_tiles, pl.sk_tiles.data(), pl.sk_tiles.size() * sizeof(GemmTile), s))) return rc;
-    if ((rc = h2d(pl.d_sk_pieces, pl.sk_pieces.data(), pl.sk_pieces.size() * sizeof(SkPiece), s))) return rc;
-    if ((rc = h2d(pl.d_sk_ranges, pl.sk_ranges.data(), pl.sk_ranges.size() * sizeof(int2), s))) return rc;
-  }
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
@@ -476,7 +406,7 @@ struct QPlan {
   Chunk* d_pack = nullptr;
   Chunk* d_sse = nullptr;
   Chunk* d_hist = nullptr;
-  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged)
+  unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged), then the cell index (kCells + 2)
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
 };
@@ -516,7 +446,7 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
   pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
-  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged);
+  pl.d_rank0 = cv.take<unsigned short>(kMaxMerged + kCells + 2);
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
@@ -684,8 +614,6 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   if ((rc = upload_admm(pl, s))) return rc;
   if (pl.ntcnt && hipMemsetAsync(pl.d_tcnt, 0, pl.ntcnt * sizeof(unsigned), s) != hipSuccess)
     return check_hip("thin counter reset");
-  if (pl.sk_ncnt && hipMemsetAsync(pl.d_sk_cnt, 0, pl.sk_ncnt * sizeof(unsigned), s) != hipSuccess)
-    return check_hip("stream-K counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
@@ -703,13 +631,9 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
-    if (pl.ntiles_small + pl.ntiles_big > 0 || pl.sk_nwg > 0) {
+    if (pl.ntiles_small + pl.ntiles_big > 0) {
       prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
-      if (pl.split)
-        launch_gemm_sk(pl.d_desc, pl.d_sk_tiles, pl.d_sk_pieces, pl.d_sk_ranges, pl.sk_nwg, pl.d_sk_part, pl.d_sk_cnt,
-                       slot, it, eps, num_attempts, s);
-      else
-        launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, false, slot, it, eps, num_attempts, s);
+      launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps, num_attempts, s);
       prof_mark(s);
     }
     if (!pl.thin.empty()) {
@@ -763,6 +687,9 @@ int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return co
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }
+int32_t admmq_debug_check_cells(int32_t n, int32_t bits, uint32_t seed, int32_t nsamp, uint32_t* maxdev) {
+  return check_cells(n, bits, seed, nsamp, maxdev);
+}
 
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
                                      int32_t bits, int32_t qscheme, int32_t num_attempts, void* workspace,

@@ -291,236 +291,6 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   }
 }
 
-// ---------------------------------------------------------------------------
-// Wide split solve, stream-K (kSolveSplit, every factor with I > kThinRows).
-//
-// Why: with the split planes the MFMA work per byte is 5x lower than in fp32, and a
-// 64 x 64 tile streams 16 KB per K-step for 64 x 64 x 32 MACs: at C3 shapes each CU
-// pulled ~1.8 MB per launch at ~55 GB/s (the per-CU fetch rate; MI355X_MICROARCH.md
-// "Indexed rows"), i.e. the GEMM was bound by per-CU bytes, not by the matrix core.
-// A 128 x 128 tile halves the bytes per MAC. 128 x 128 tiles are too few and too
-// uneven to fill 256 CUs (the three R = 1141 layers are 76 % of a resnet18 mode), so
-// the K-steps of ALL tiles of the launch form one sequence that is cut into equal
-// contiguous ranges, one per workgroup (stream-K): every CU gets the same number of
-// K-steps. A tile cut by a range boundary is computed as pieces; each piece stores its
-// fp32 partial tile, and the last piece to arrive sums the partials in piece order
-// (deterministic: the same sums in the same order whoever arrives last) and runs the
-// epilogue. Workgroup b runs on XCD b % 8 (round-robin dispatch): b is mapped to the
-// logical range (b % 8) (nwg / 8) + b / 8, so each XCD takes one contiguous eighth of
-// the step sequence and its tiles share operand panels in that XCD's L2.
-//
-// 512 threads: wave w owns rows 32 (w & 3) .. +32 and columns 64 (w >> 2) .. +64 of
-// the tile (two 32 x 32 accumulators). Operand image, swizzle and fragment order as
-// k_gemm's split form; NS-deep LDS-DMA ring (32 KB per stage), drained between pieces.
-// Rows past Ip and columns past ldm read a clamped (valid) row; such outputs are never
-// stored.
-template <int NS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_sk(
-    const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, const SkPiece* __restrict__ pieces,
-    const int2* __restrict__ ranges, float* __restrict__ part, unsigned* __restrict__ cnt, int slot, int iter,
-    float eps, int ncand) {
-  constexpr int NW = 8, NT = 512;
-  constexpr int ROWS = 256;                    // image rows per stage: A (128) then B (128)
-  constexpr int STAGE = ROWS * 32;             // floats per stage (128 B per row)
-  constexpr int GPW = ROWS / 8 / NW;           // glds wave-instructions per wave per stage (8 rows each)
-  constexpr int SLAB = 128 * 128;              // floats per partial tile
-  static_assert(NS >= 2 && NS <= 4, "NS");
-  __shared__ __attribute__((aligned(16))) float st0[STAGE];
-  __shared__ __attribute__((aligned(16))) float st1[STAGE];
-  __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
-  __shared__ __attribute__((aligned(16))) float st3[NS > 3 ? STAGE : 4];
-  float* const stp[4] = {st0, st1, st2, st3};
-  __shared__ unsigned red[3][NW + 1];          // red[0][NW]: "last piece" broadcast
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;
-  const int i = lane & 31, h = lane >> 5;
-  const int swz = (i >> 1) & 7;
-  const int aoff = (32 * wm + i) * 32, boff = (128 + 64 * wn + i) * 32;
-  const int L = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  const int2 rg = ranges[L];
-
-  for (int q = 0; q < rg.y; ++q) {
-    const SkPiece pc = pieces[rg.x + q];
-    const GemmTile tl = tiles[pc.tile];
-    const ProbDesc& p = probs[tl.prob];
-    const int ld = tl.ld, ldm = tl.ldm, Ip = tl.pad_;
-    const int row0 = tl.tm * 128, col0 = tl.tn * 128;
-    const int n = pc.k1 - pc.k0;
-    const float* src[GPW];
-#pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const int g = wave * GPW + j;
-      const int r = 8 * g + (lane >> 3);                       // image row
-      const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
-      src[j] = (r < 128) ? tl.P + (size_t)min(row0 + r, Ip - 1) * ld + 4 * c
-                         : tl.M + (size_t)min(col0 + r - 128, ldm - 1) * ldm + 4 * c;
-      src[j] += (size_t)pc.k0 * BK;
-    }
-#define ADMMQ_SK_ISSUE(s, kt)                                              \
-  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
-    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s) ADMMQ_SK_ISSUE(s, min(s, n - 1));
-    bool skip = p.flags[0] != 0;
-    if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
-      if (pc.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
-      skip = true;
-    }
-    if (skip) {   // uniform over the problem's pieces (the flag / residuals of the previous iteration)
-      wait_vmcnt<0>();
-      __syncthreads();
-      continue;
-    }
-    if (pc.first) {   // this iteration's quantizer-search accumulators start at zero
-      unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
-      unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
-      unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
-      for (int c = tid; c < ncand; c += NT) sse[c] = 0ull;
-      for (int c = tid; c < kHistRep * (ncand + 1); c += NT) { h1[c] = 0ull; h2[c] = 0ull; }
-      if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
-    }
-    f32x16 acc0, acc1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
-#define ADMMQ_SK_STEP(s, kt)                                                                  \
-  do {                                                                                        \
-    wait_vmcnt<GPW * (NS - 2)>();                                                             \
-    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
-    raw_barrier();                                                                            \
-    ADMMQ_SK_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, n - 1));                           \
-    const float* st = stp[s];                                                                 \
-    _Pragma("unroll") for (int kc = 0; kc < 2; ++kc) {                                        \
-      const int ch = ((2 * kc + h) ^ swz) * 4, cl = ((4 + 2 * kc + h) ^ swz) * 4;             \
-      const f16x8 ah = as_h8(*reinterpret_cast<const float4*>(st + aoff + ch));               \
-      const f16x8 al = as_h8(*reinterpret_cast<const float4*>(st + aoff + cl));               \
-      const f16x8 bh0 = as_h8(*reinterpret_cast<const float4*>(st + boff + ch));              \
-      const f16x8 bl0 = as_h8(*reinterpret_cast<const float4*>(st + boff + cl));              \
-      const f16x8 bh1 = as_h8(*reinterpret_cast<const float4*>(st + boff + 1024 + ch));       \
-      const f16x8 bl1 = as_h8(*reinterpret_cast<const float4*>(st + boff + 1024 + cl));       \
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0, acc0, 0, 0, 0);                  \
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1, acc1, 0, 0, 0);                  \
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0, acc0, 0, 0, 0);                  \
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1, acc1, 0, 0, 0);                  \
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0, acc0, 0, 0, 0);                  \
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1, acc1, 0, 0, 0);                  \
-    }                                                                                         \
-  } while (0)
-    const int nfull = n / NS * NS;
-    for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) ADMMQ_SK_STEP(s, kt0 + s);
-    }
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-      if (nfull + s < n) ADMMQ_SK_STEP(s, nfull + s);
-#undef ADMMQ_SK_STEP
-#undef ADMMQ_SK_ISSUE
-    wait_vmcnt<0>();
-    __syncthreads();   // nothing in flight; every wave is past its last stage read
-
-    if (pc.np > 1) {   // partial tile -> slab pidx; the last piece to arrive combines
-      typedef __attribute__((address_space(1))) f32x4 gst4;
-      float* slab = part + (size_t)(pc.part + pc.pidx) * SLAB;
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        *(gst4*)(slab + ((size_t)((wave * 2 + 0) * 4 + r4) * 64 + lane) * 4) =
-            f32x4{acc0[4 * r4], acc0[4 * r4 + 1], acc0[4 * r4 + 2], acc0[4 * r4 + 3]};
-        *(gst4*)(slab + ((size_t)((wave * 2 + 1) * 4 + r4) * 64 + lane) * 4) =
-            f32x4{acc1[4 * r4], acc1[4 * r4 + 1], acc1[4 * r4 + 2], acc1[4 * r4 + 3]};
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(cnt + pc.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = old + 1 == (unsigned)pc.np;
-        if (last) {
-          __hip_atomic_store(cnt + pc.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        red[0][NW] = last;
-      }
-      __syncthreads();
-      if (!red[0][NW]) continue;   // (the loop's next piece starts with no LDS / global traffic pending)
-      // fixed-order sum of every piece's slab (own included, read back): deterministic
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
-      for (int j = 0; j < pc.np; ++j) {
-        const float* sl = part + (size_t)(pc.part + j) * SLAB;
-        float4 v0[4], v1[4];
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          v0[r4] = gld4(sl + ((size_t)((wave * 2 + 0) * 4 + r4) * 64 + lane) * 4);
-          v1[r4] = gld4(sl + ((size_t)((wave * 2 + 1) * 4 + r4) * 64 + lane) * 4);
-        }
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          acc0[4 * r4] += v0[r4].x; acc0[4 * r4 + 1] += v0[r4].y; acc0[4 * r4 + 2] += v0[r4].z; acc0[4 * r4 + 3] += v0[r4].w;
-          acc1[4 * r4] += v1[r4].x; acc1[4 * r4 + 1] += v1[r4].y; acc1[4 * r4 + 2] += v1[r4].z; acc1[4 * r4 + 3] += v1[r4].w;
-        }
-      }
-    }
-
-    // epilogue: H_T = acc 2^-(eP_row + eM_col); X = H_T - U stats over the valid region
-    {
-      const int colb = col0 + 64 * wn + i;
-      int ecol[2];
-      float uv[2][16];
-      int erow[16];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) ecol[c] = gld_i32(tl.eM + min(colb + 32 * c, ldm - 1));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = min(row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h, Ip - 1);
-        erow[r] = gld_i32(tl.eP + row);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) uv[c][r] = ldg(tl.U + (size_t)row * ld + min(colb + 32 * c, ld - 1));
-      }
-      unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int col = colb + 32 * c;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float a = c == 0 ? acc0[r] : acc1[r];
-          const float ht = __builtin_ldexpf(a, -(erow[r] + ecol[c]));
-          const float x = ht - uv[c][r];
-          if (row < Ip && col < ld) {
-            const size_t off = (size_t)row * ld + col;
-            p.HT[off] = ht;
-            if (p.X_dbg) p.X[off] = x;   // debug output only (readers re-form X = H_T - U)
-          }
-          if (row < p.I && col < p.R) {
-            amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
-            const unsigned e = enc_ord(x);
-            mn = min(mn, e);
-            mxo = max(mxo, e);
-          }
-        }
-      }
-      amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
-      if (lane == 0) { red[0][wave] = amax; red[1][wave] = mn; red[2][wave] = mxo; }
-      __syncthreads();
-      if (tid == 0) {
-        unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
-        unsigned* stt = p.mv.stat + 4 * slot;
-        atomicMax(&stt[0], a0);
-        atomicMin(&stt[1], a1);
-        atomicMax(&stt[2], a2);
-      }
-      __syncthreads();   // red is reused by the next piece
-    }
-  }
-}
-
 // One block per (problem, row): rows [0, Ip) of P (fp32, padded, zero pads) -> P2 / eP.
 // `which` 0: P of every split problem; 1: M (rows [0, ldm)) -> M2 / eM.
 __global__ __launch_bounds__(256) void k_split_rows(const ProbDesc* __restrict__ probs, int which) {
@@ -768,22 +538,22 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
                  int iter, float eps, int ncand, hipStream_t s) {
-  // fp32 form (the split form runs on k_gemm_sk): tiles[0 .. ntiles_big) are 64x64
-  // (WM = 2, one wave per 32x32 sub-tile, 3-deep ring), then ntiles_small 32x64 tiles
-  // (WM = 1: the 17..32-row factors, 2 waves per sub-tile splitting each K-step, 4-deep ring)
-  (void)split;
-  if (ntiles_big > 0)
-    hipLaunchKernelGGL((k_gemm<2, 1, 3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
-  if (ntiles_small > 0)
-    hipLaunchKernelGGL((k_gemm<1, 2, 4, false>), dim3(ntiles_small), dim3(256), 0, s, d, tiles + ntiles_big, slot,
-                       iter, eps, ncand);
-}
-
-void launch_gemm_sk(const ProbDesc* d, const GemmTile* tiles, const SkPiece* pieces, const int2* ranges, int nwg,
-                    float* part, unsigned* cnt, int slot, int iter, float eps, int ncand, hipStream_t s) {
-  if (nwg > 0)
-    hipLaunchKernelGGL((k_gemm_sk<4>), dim3(nwg), dim3(512), 0, s, d, tiles, pieces, ranges, part, cnt, slot, iter, eps,
-                       ncand);
+  // tiles[0 .. ntiles_big) are 64x64 (WM = 2, one wave per 32x32 sub-tile, 3-deep ring),
+  // then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors, 2 waves per sub-tile
+  // splitting each K-step, 4-deep ring)
+  if (ntiles_big > 0) {
+    if (split)
+      hipLaunchKernelGGL((k_gemm<2, 1, 3, true>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
+    else
+      hipLaunchKernelGGL((k_gemm<2, 1, 3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
+  }
+  if (ntiles_small > 0) {
+    const GemmTile* t = tiles + ntiles_big;
+    if (split)
+      hipLaunchKernelGGL((k_gemm<1, 2, 4, true>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
+    else
+      hipLaunchKernelGGL((k_gemm<1, 2, 4, false>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
+  }
 }
 
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,

@@ -126,6 +126,43 @@ __global__ void k_check_thresholds(unsigned seed, int nsamp, unsigned* mismatche
     if (level_threshold_fast(s, k) != level_threshold(s, k)) atomicAdd(mismatches, 1u);
   }
 }
+// Diagnostics: the host's cell lower bound (merged_tables, h3_setup) holds for random mx
+// in the range it is used for: every threshold e's actual cell is at most
+// floor(z_e (1 + 1e-4)), the cell the host counts it below. Also reports the largest
+// deviation of a cell position from its key proportion (in cells x 1e6).
+__global__ void k_check_cells(int n, int qmax, unsigned seed, int nsamp, unsigned* bad, unsigned* maxdev) {
+  const int M = qmax * n;
+  const double kmax = (double)(2 * qmax - 1) * (double)(6LL * (n - 1));
+  const float den = (float)(2 * qmax - 1);
+  for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < (long long)nsamp * M;
+       w += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(w / M), e = (int)(w - (long long)i * M);
+    unsigned x = seed ^ (0x9E3779B9u * (unsigned)(i + 1));
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    const float mx = __uint_as_float((x & 0x007FFFFFu) | ((27u + (x >> 23) % 201u) << 23));   // [2^-100, 2^101)
+    if (!(mx >= 0x1p-100f && mx <= 0x1p100f)) continue;
+    const int k = 1 + e / n, c = e - (k - 1) * n;
+    const float v = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
+    const float inv = (float)kCells / level_threshold_fast((2.0f * cand_t(mx, n - 1, n)) / den, qmax);
+    const int ca = min(kCells - 1, (int)(v * inv));
+    const double z = (double)kCells * ((double)(2 * k - 1) * (double)((n - 1) + 5LL * c)) / kmax;
+    if ((double)ca > floor(z * (1.0 + 1e-4))) atomicAdd(bad, 1u);
+    const double dev = fabs((double)v * (double)inv - z);
+    atomicMax(maxdev, (unsigned)fmin(dev * 1e6, 4e9));
+  }
+}
+int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out) {
+  unsigned* d = nullptr;
+  if (hipMalloc(&d, 2 * sizeof(unsigned)) != hipSuccess) return -1;
+  (void)hipMemset(d, 0, 2 * sizeof(unsigned));
+  hipLaunchKernelGGL(k_check_cells, dim3(512), dim3(256), 0, 0, n, 1 << (bits - 1), seed, nsamp, d, d + 1);
+  unsigned h[2] = {0u, 0u};
+  const bool ok = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(d);
+  if (maxdev_out) *maxdev_out = h[1];
+  return ok ? (int)h[0] : -1;
+}
+
 int check_thresholds(unsigned seed, int nsamp) {
   unsigned* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return -1;
@@ -415,7 +452,11 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
     }
   };
   if (!last) { trace(T3); return; }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // every byte handed over by the other blocks (h1/h2 replicas, s2) was written by
+  // memory-side atomics drained before the ticket and is read below by agent-scope
+  // (sc1) atomic loads only, so no L1 invalidate is needed (cdna_hip_programming.md
+  // Guideline 16, sc1 consumer); the wavefront fence only keeps the loads after the ticket
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   unsigned long long* H1 = h1;                                            // reuse LDS: n+1 each
   unsigned long long* H2 = reinterpret_cast<unsigned long long*>(thr);
   for (int b = threadIdx.x; b <= n; b += blockDim.x) {
@@ -460,7 +501,6 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
 // A coarse index cnt[g] = #{thresholds in cells < g} over kCells equal cells of
 // [0, max threshold] then turns B(a) into two independent LDS reads and a walk of
 // the few thresholds of a's cell.
-constexpr int kCells = 4096;
 constexpr int kH3Threads = 512;       // k_mse_hist3 block (its helpers take the size as a constant:
 constexpr int kSmallThreads = 1024;   // k_mse_small_admm block  reading blockDim is a global load)
 
@@ -647,16 +687,36 @@ __device__ __forceinline__ void h3_load_order(const unsigned short* __restrict__
 // Stage-1 table of one job in LDS (the setup of k_mse_hist3 and k_mse_small_admm): the
 // thresholds in the host's merged order with the tie groups ordered by value, L per
 // (level, candidate), the coarse cell index; the buckets zeroed. Returns the cell scale.
+//
+// L and the cell index come almost entirely from the host (they do not depend on mx):
+// distinct keys give distinct thresholds, so L = rank + 1 outside the tie groups, and
+// cells_g[g] (after the kMaxMerged rank entries of the host order) is a LOWER bound of
+// #{thresholds in cells < g} valid for every mx: the host counts the thresholds whose
+// key puts them below cell g with a 1e-4 relative margin (the thresholds are within a
+// few ulps of their key's proportion of the largest one). h3_insert_n starts each
+// element's search there and walks up to the exact count. If the host order does not
+// hold for this mx (never observed), everything is derived in the block instead.
 template <int QMAX>
 __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
                                          const unsigned short* __restrict__ groups, int ngroups,
+                                         const unsigned short* __restrict__ cells_g,
                                          unsigned long long* sumA, unsigned long long* sumN, unsigned* cntA,
                                          unsigned* cntN, float* thr, float* tsort, unsigned short* rnk,
                                          unsigned short* cell, int nt) {
   const int M = QMAX * n;
   const int nb = M + 1 + 64;
   ADMMQ_SETUP_STAMP(0);
-  // thresholds, each also scattered to its host-order rank (kR0 * nt >= kMaxMerged >= M)
+  // the host cell index (kCells + 1 entries as u32 pairs), issued first: used only at
+  // the end of the setup
+  constexpr int kCellWords = (kCells + 2) / 2;
+  const unsigned* cw = reinterpret_cast<const unsigned*>(cells_g);
+  unsigned cv[(kCellWords + 511) / 512];
+  const int ncw = (kCellWords + nt - 1) / nt;
+#pragma unroll
+  for (int j = 0; j < (kCellWords + 511) / 512; ++j)
+    if (j < ncw) cv[j] = gld_u32(cw + min((int)threadIdx.x + j * nt, kCellWords - 1));
+  // thresholds, each also scattered to its host-order rank (kR0 * nt >= kMaxMerged >= M);
+  // L = rank + 1 (tie groups below)
   const float den = (float)(2 * QMAX - 1);
 #pragma unroll
   for (int j = 0; j < kR0; ++j) {
@@ -666,15 +726,15 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
       const float v = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
       thr[e] = v;
       tsort[pre.r0v[j]] = v;
-      rnk[e] = pre.r0v[j];
+      rnk[e] = (unsigned short)(pre.r0v[j] + 1);
     }
   }
   for (int i = threadIdx.x; i < nb; i += nt) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
   __syncthreads();
   ADMMQ_SETUP_STAMP(1);
-  // exact-key ties: order by actual value (the thread's first group was prefetched; a
-  // load in the same loop would, after the join, make the compiler wait for every
-  // outstanding load, the elements included)
+  // exact-key ties: order by actual value, L = 1 + index of the last equal value (the
+  // thread's first group was prefetched; a load in the same loop would, after the join,
+  // make the compiler wait for every outstanding load, the elements included)
   auto tie_group = [&](const unsigned short* gr) {
     const int r0 = gr[0], m = gr[1];
     int es[4];
@@ -685,7 +745,12 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
         const float tv = vs[j]; vs[j] = vs[j - 1]; vs[j - 1] = tv;
         const int te = es[j]; es[j] = es[j - 1]; es[j - 1] = te;
       }
-    for (int j = 0; j < m; ++j) { tsort[r0 + j] = vs[j]; rnk[es[j]] = (unsigned short)(r0 + j); }
+    for (int j = 0; j < m; ++j) {
+      int l = j;
+      while (l + 1 < m && vs[l + 1] == vs[j]) ++l;
+      tsort[r0 + j] = vs[j];
+      rnk[es[j]] = (unsigned short)(r0 + l + 1);
+    }
   };
   if ((int)threadIdx.x < ngroups) {
     const unsigned short gr[6] = {(unsigned short)(pre.gw[0] & 0xFFFFu), (unsigned short)(pre.gw[0] >> 16),
@@ -695,35 +760,33 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
   }
   if (ngroups > nt)
     for (int g = threadIdx.x + nt; g < ngroups; g += nt) tie_group(groups + 6 * g);
+  // the host cell index into LDS
+  unsigned* cell32 = reinterpret_cast<unsigned*>(cell);
+#pragma unroll
+  for (int j = 0; j < (kCellWords + 511) / 512; ++j) {
+    const int i = threadIdx.x + j * nt;
+    if (j < ncw && i < kCellWords) cell32[i] = cv[j];
+  }
   __syncthreads();
   ADMMQ_SETUP_STAMP(2);
-  // one pass over the sorted table: the order check, L = 1 + index of the last equal
-  // value, and the coarse index cell(v) = min(kCells-1, (int)(v * inv)) (non-decreasing
-  // in v, so thresholds in cells below cell(a) are < a and those above are > a)
-  const float inv = (float)kCells / tsort[M - 1];
-  auto fill_cells = [&](float iv) {
+  // the order check (sorted thresholds non-decreasing); the cell scale from the largest
+  // threshold (level QMAX of the last candidate), computed directly
+  int bad = 0;
+  for (int r = threadIdx.x; r + 1 < M; r += nt) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
+  const float inv = (float)kCells / level_threshold_fast((2.0f * cand_t(mx, n - 1, n)) / den, QMAX);
+  // the host bound assumes normal-range thresholds (relative rounding): elsewhere, exact cells
+  bad |= (mx >= 0x1p-100f && mx <= 0x1p100f) ? 0 : 1;
+  if (__syncthreads_or(bad)) {   // never expected: rank by counting, exact cells (exact either way)
+    rank_by_counting(thr, tsort, rnk, mx, n, QMAX);
+    __syncthreads();
+    const float inv2 = (float)kCells / tsort[M - 1];
     for (int r = threadIdx.x; r < M; r += nt) {
-      const int cr = min(kCells - 1, (int)(tsort[r] * iv));
-      const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * iv));
+      const int cr = min(kCells - 1, (int)(tsort[r] * inv2));
+      const int cp = r == 0 ? -1 : min(kCells - 1, (int)(tsort[r - 1] * inv2));
       for (int g = cp + 1; g <= cr; ++g) cell[g] = (unsigned short)r;
       if (r == M - 1)
         for (int g = cr + 1; g <= kCells; ++g) cell[g] = (unsigned short)M;
     }
-  };
-  int bad = 0;
-  for (int r = threadIdx.x; r + 1 < M; r += nt) bad |= (tsort[r] > tsort[r + 1]) ? 1 : 0;
-  for (int e = threadIdx.x; e < M; e += nt) {
-    const int r = rnk[e];
-    int l = r + 1;
-    while (l < M && tsort[l] == tsort[r]) ++l;
-    rnk[e] = (unsigned short)l;
-  }
-  fill_cells(inv);
-  if (__syncthreads_or(bad)) {   // never expected: rank by counting, then the cells again (exact either way)
-    rank_by_counting(thr, tsort, rnk, mx, n, QMAX);
-    __syncthreads();
-    const float inv2 = (float)kCells / tsort[M - 1];
-    fill_cells(inv2);
     __syncthreads();
     ADMMQ_SETUP_STAMP(3);
     ADMMQ_SETUP_STAMP(4);
@@ -736,7 +799,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
 
 // Buckets B = #{thresholds <= |x|} of N elements and their LDS histogram adds, in phases whose LDS reads are independent across the
 // elements (so their latencies overlap instead of chaining element after element): the
-// two cell bounds, then three threshold probes, then the walk for an element whose cell
+// cell's lower bound, then three threshold probes, then the walk for an element whose cell
 // still holds more thresholds <= |x| (rare), then the histogram adds.
 template <int N>
 __device__ __forceinline__ void h3_insert_n(const float* xs, float inv, const float* tsort, const unsigned short* cell,
@@ -745,11 +808,11 @@ __device__ __forceinline__ void h3_insert_n(const float* xs, float inv, const fl
   float a[N];
   int B[N], hi[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
+  for (int j = 0; j < N; ++j) {   // start at the cell's lower bound (h3_setup); the upper bound is M
     a[j] = __builtin_fabsf(xs[j]);
     const int g = min(kCells - 1, (int)(a[j] * inv));
     B[j] = cell[g];
-    hi[j] = cell[g + 1];
+    hi[j] = M;
   }
   bool more[N];
 #pragma unroll
@@ -953,7 +1016,8 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   __shared__ unsigned long long wtot[8], wtot2[8];
   __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
-  const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell, kH3Threads);
+  const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, rank0 + kMaxMerged, sumA, sumN, cntA, cntN, thr, tsort,
+                                   rnk, cell, kH3Threads);
   const unsigned long long T1 = ADMMQ_NOW();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
@@ -1009,7 +1073,11 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
     }
   };
   if (!last) { trace(T3); return; }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // every byte handed over by the other blocks (h1/h2 replicas, s2) was written by
+  // memory-side atomics drained before the ticket and is read below by agent-scope
+  // (sc1) atomic loads only, so no L1 invalidate is needed (cdna_hip_programming.md
+  // Guideline 16, sc1 consumer); the wavefront fence only keeps the loads after the ticket
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
   const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
   __shared__ int lsel[2 + kMaxSel];
@@ -1114,7 +1182,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
     float* tsort = thr + M;
     unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);
     unsigned short* cell = rnk + ((M + 1) & ~1);
-    const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, sumA, sumN, cntA, cntN, thr, tsort, rnk, cell, kSmallThreads);
+    const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, rank0 + kMaxMerged, sumA, sumN, cntA, cntN, thr,
+                                     tsort, rnk, cell, kSmallThreads);
     // the stop test after the (LDS-only) setup: tested earlier, the compiler would sink
     // the element loads below it and their latency would no longer overlap the setup
     if (stopped) return;   // converged earlier (sticky break)

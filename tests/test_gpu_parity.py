@@ -363,3 +363,19 @@ def test_level_threshold_closed_form(torch_dev):
     lib = _lib.load()
     for seed in (1, 2, 3, 4):
         assert lib.admmq_debug_check_thresholds(seed, 1 << 20) == 0
+
+
+@pytest.mark.parametrize("n,bits", [(2, 2), (7, 6), (50, 4), (200, 4), (200, 6), (1000, 2), (1024, 3), (512, 4)])
+def test_stage1_host_cell_bound(torch_dev, n, bits):
+    """The host's mx-independent lower bound of the stage-1 cell index (merged_tables,
+    h3_setup) holds: for random mx in [2^-100, 2^100], every merged threshold lies at or
+    below the cell the host counts it under; the largest deviation of a threshold's cell
+    position from its key proportion is reported (the bound allows 1e-4 relative)."""
+    import ctypes
+    from admmq import _lib
+    lib = _lib.load()
+    dev = ctypes.c_uint32(0)
+    for seed in (11, 12):
+        assert lib.admmq_debug_check_cells(n, bits, seed, 2048, ctypes.byref(dev)) == 0
+    print(f"n={n} bits={bits}: max deviation {dev.value * 1e-6:.2e} cells")
+    assert dev.value * 1e-6 < 0.05

@@ -44,6 +44,28 @@ class CpLayer(ctypes.Structure):
 
 
 _lib = None
+OPS_PATH = os.path.join(_HERE, "libadmmq_torch.so")
+_ops = None
+
+
+def use_ops() -> bool:
+    """The drop-ins route through torch.ops.admmq (libadmmq_torch.so over the C-ABI),
+    except when ADMMQ_LIB selects another build of the C-ABI library for diagnostics
+    (the op library links the default one): then they call the C-ABI through ctypes."""
+    return not os.environ.get("ADMMQ_LIB")
+
+
+def ops():
+    """``torch.ops.admmq`` (csrc/torch_ops.cpp): loads libadmmq_torch.so once and raises
+    loudly when it was not built - there is no CPU fallback."""
+    global _ops
+    if _ops is None:
+        if not os.path.exists(OPS_PATH):
+            raise ImportError(f"admmq: {OPS_PATH} is missing - build it with `make -C admm-quantization_amd/csrc`")
+        load()
+        torch.ops.load_library(OPS_PATH)
+        _ops = torch.ops.admmq
+    return _ops
 
 
 def load() -> ctypes.CDLL:

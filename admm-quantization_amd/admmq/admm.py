@@ -91,15 +91,34 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     Returns the list of new H tensors (and the caller's U tensors are updated in
     place). With ``return_info`` also returns an int32 tensor [n, 4] of
     {iterations run, converged, spd_error, 0}; with ``debug_outputs`` a list of
-    (H_T, X) of the last iteration per problem.
+    (H_T, X) of the last iteration per problem. Calls ``torch.ops.admmq.admm_iteration_batched``
+    (csrc/torch_ops.cpp), which calls ``admmq_admm_prepare`` / ``admmq_admm_run``.
     """
-    lib = _lib.load()
     if len(problems) == 0:
         return []
     for (H, U, F, G) in problems:
         _lib.require_device(H, U, F, G)
         if H.dim() != 2:
             raise ValueError("admm_iteration expects 2-D factors (I, R)")
+    code = _scheme_code(qscheme)
+    if not _lib.use_ops():
+        return _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd,
+                                            debug_outputs, return_info)
+    Hs, Us, Fs, Gs = (list(x) for x in zip(*problems))
+    outs, info, hts, xs = _lib.ops().admm_iteration_batched(Hs, Us, Fs, Gs, int(max_iter), float(eps), int(bits), code,
+                                                            int(num_attempts), bool(check_spd), bool(debug_outputs))
+    ret = [list(outs) if max_iter > 1 else [p[0] for p in problems]]   # max_iter <= 1: the input H objects
+    if debug_outputs:
+        ret.append(list(zip(hts, xs)))
+    if return_info:
+        ret.append(info)
+    return ret[0] if len(ret) == 1 else tuple(ret)
+
+
+def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd, debug_outputs,
+                                 return_info):
+    """The same call through the C-ABI with ctypes (diagnostic builds, cross-checks)."""
+    lib = _lib.load()
     dev = problems[0][0].device
     Hs = [p[0].contiguous() for p in problems]
     Fs = [p[2].contiguous() for p in problems]
@@ -127,7 +146,6 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     if max_iter <= 1:
         outs = [p[0] for p in problems]
         return (outs, info.view(n, 4)) if return_info else outs
-    code = _scheme_code(qscheme)
     outs = [torch.empty_like(h) for h in Hs]
     for it, o in zip(items, outs):
         it.H_out = o.data_ptr()

@@ -50,6 +50,15 @@ def gram_mttkrp_batched(layers: Sequence[Tuple[torch.Tensor, Sequence[torch.Tens
     """``[(G, F)]`` for mode ``mode`` of every ``(W, factors)`` (factors[mode] is not read)."""
     if not layers:
         return []
+    if _lib.use_ops():   # torch.ops.admmq.cp_gram_mttkrp (csrc/torch_ops.cpp) -> admmq_cp_gram_mttkrp
+        for W, fs in layers:
+            if len(fs) != W.dim():
+                raise ValueError(f"admmq: {W.dim()}-way tensor needs {W.dim()} factors, got {len(fs)}")
+            if not 0 <= mode < W.dim():
+                raise ValueError(f"admmq: mode {mode} out of range for a {W.dim()}-way tensor")
+            _lib.require_device(W, *fs)
+        G, F = _lib.ops().cp_gram_mttkrp([W for W, _ in layers], [f for _, fs in layers for f in fs], int(mode))
+        return list(zip(G, F))
     lib = _lib.load()
     keep, outs, descs = [], [], []
     for W, fs in layers:
@@ -87,6 +96,13 @@ def rel_error_batched(layers: Sequence[Tuple[torch.Tensor, Sequence[torch.Tensor
     fp64 results on the device and does not sync."""
     if not layers:
         return torch.zeros(0, dtype=torch.float64) if as_tensor else []
+    if _lib.use_ops():   # torch.ops.admmq.cp_rel_error (csrc/torch_ops.cpp) -> admmq_cp_rel_error
+        for W, fs in layers:
+            if len(fs) != W.dim():
+                raise ValueError(f"admmq: {W.dim()}-way tensor needs {W.dim()} factors, got {len(fs)}")
+            _lib.require_device(W, *fs)
+        out = _lib.ops().cp_rel_error([W for W, _ in layers], [f for _, fs in layers for f in fs])
+        return out if as_tensor else [float(v) for v in out.cpu()]
     lib = _lib.load()
     keep, descs = [], []
     for W, fs in layers:

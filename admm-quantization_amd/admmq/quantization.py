@@ -59,6 +59,10 @@ def quantize_batched(tensors: Sequence[torch.Tensor], bits: int, qscheme: str, n
         if t.numel() == 0:
             raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
         xs.append(t.contiguous())
+    if _lib.use_ops():   # torch.ops.admmq.quantize_batched (csrc/torch_ops.cpp) -> admmq_quantize_batched
+        has_kw = code == 3 and tmin is not None and tmax is not None
+        return list(_lib.ops().quantize_batched(xs, int(bits), code, int(num_attempts),
+                                                float(tmin) if has_kw else None, float(tmax) if has_kw else None))
     dev = xs[0].device
     outs = [torch.empty_like(x) for x in xs]
     items = []

@@ -21,8 +21,7 @@ import torch
 from . import _lib
 
 
-def _layer(W: torch.Tensor, factors: Sequence[torch.Tensor], G: Optional[torch.Tensor] = None,
-           F: Optional[torch.Tensor] = None) -> _lib.CpLayer:
+def _validate(W: torch.Tensor, factors: Sequence[torch.Tensor]):
     if W.dim() not in (2, 3):
         raise ValueError(f"admmq: CP layer tensor must be 2-D or 3-D, got {W.dim()}-D")
     if len(factors) != W.dim():
@@ -32,6 +31,12 @@ def _layer(W: torch.Tensor, factors: Sequence[torch.Tensor], G: Optional[torch.T
         if f.dim() != 2 or f.shape != (W.shape[d], R):
             raise ValueError(f"admmq: factor {d} has shape {tuple(f.shape)}, expected {(W.shape[d], R)}")
     _lib.require_device(W, *factors)
+    return R
+
+
+def _layer(W: torch.Tensor, factors: Sequence[torch.Tensor], G: Optional[torch.Tensor] = None,
+           F: Optional[torch.Tensor] = None) -> _lib.CpLayer:
+    R = _validate(W, factors)
     L = _lib.CpLayer()
     L.W = W.data_ptr()
     for d in range(3):
@@ -52,11 +57,9 @@ def gram_mttkrp_batched(layers: Sequence[Tuple[torch.Tensor, Sequence[torch.Tens
         return []
     if _lib.use_ops():   # torch.ops.admmq.cp_gram_mttkrp (csrc/torch_ops.cpp) -> admmq_cp_gram_mttkrp
         for W, fs in layers:
-            if len(fs) != W.dim():
-                raise ValueError(f"admmq: {W.dim()}-way tensor needs {W.dim()} factors, got {len(fs)}")
+            _validate(W, fs)
             if not 0 <= mode < W.dim():
                 raise ValueError(f"admmq: mode {mode} out of range for a {W.dim()}-way tensor")
-            _lib.require_device(W, *fs)
         G, F = _lib.ops().cp_gram_mttkrp([W for W, _ in layers], [f for _, fs in layers for f in fs], int(mode))
         return list(zip(G, F))
     lib = _lib.load()
@@ -98,9 +101,7 @@ def rel_error_batched(layers: Sequence[Tuple[torch.Tensor, Sequence[torch.Tensor
         return torch.zeros(0, dtype=torch.float64) if as_tensor else []
     if _lib.use_ops():   # torch.ops.admmq.cp_rel_error (csrc/torch_ops.cpp) -> admmq_cp_rel_error
         for W, fs in layers:
-            if len(fs) != W.dim():
-                raise ValueError(f"admmq: {W.dim()}-way tensor needs {W.dim()} factors, got {len(fs)}")
-            _lib.require_device(W, *fs)
+            _validate(W, fs)
         out = _lib.ops().cp_rel_error([W for W, _ in layers], [f for _, fs in layers for f in fs])
         return out if as_tensor else [float(v) for v in out.cpu()]
     lib = _lib.load()

@@ -92,6 +92,7 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_legacy_stage1": (I32, [I32]),
         "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
         "admmq_debug_check_thresholds": (I32, [ctypes.c_uint32, I32]),
+        "admmq_debug_set_fused_finalize": (I32, [I32]),
         "admmq_debug_check_cells": (I32, [I32, I32, ctypes.c_uint32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
         "admmq_profile_end": (I32, [P, P]),
@@ -187,6 +188,23 @@ class solve_mode:
 
     def __exit__(self, *exc):
         load().admmq_set_solve_mode(self.prev)
+        return False
+
+
+class fused_finalize:
+    """Context manager: run the big jobs' finalize step inside the search launch
+    (default, where all of its blocks are resident) or as its own launch. Same
+    integers; used as a cross-check in the parity tests. Restores the default on exit."""
+
+    def __init__(self, enable: bool):
+        self.enable = enable
+
+    def __enter__(self):
+        load().admmq_debug_set_fused_finalize(1 if self.enable else 0)
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_fused_finalize(1)
         return False
 
 

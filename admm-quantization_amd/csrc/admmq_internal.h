@@ -57,6 +57,7 @@ struct MseView {
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
   unsigned* ticket;            // [slot] stage-1 blocks finished (the last one runs the selection)
+  unsigned* ready;             // [slot] fused finalize: iteration + 1 once the selection is published
   const int* done;             // early-exit flag (ADMM) or nullptr
   int nhist, pad_;             // stage-1 blocks of this job
 };
@@ -193,7 +194,9 @@ int check_thresholds(unsigned seed, int nsamp);
 int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out);
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
-                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s);
+                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
+                      hipStream_t s);
+int hist3_fin_capacity(int ncand, int bits, int nv);
 int small_admm_groups(long long maxtotal);
 void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ngr, int ncand, int bits, int slot,
                            int iter, const unsigned short* rank0, const unsigned short* groups, int ngroups,

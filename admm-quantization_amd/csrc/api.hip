@@ -63,6 +63,9 @@ static Prof g_prof;
 static std::atomic<bool> g_exhaustive{false};
 static std::atomic<bool> g_legacy_stage1{false};
 static std::atomic<int> g_solve_mode{kSolveSplit};
+// fused finalize (k_mse_hist3<.., true>) where the residency check allows it; 0: the
+// separate k_finalize_admm launch (A/B and cross-check, same integers)
+static std::atomic<bool> g_fused_finalize{true};
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
@@ -140,6 +143,7 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
   v.ticket = cv.take<unsigned>((size_t)nslot);
+  v.ready = cv.take<unsigned>((size_t)nslot);
 
 }
 
@@ -167,6 +171,8 @@ struct AdmmPlan {
   std::vector<int> small;         // jobs with I <= kThinRows (one-block fused search + finalize)
   int* d_small = nullptr;
   int nfin_big = 0, nhist_big = 0;   // finalize / stage-1 units of the other jobs (listed first)
+  bool rows_aligned = true;          // every big job's stage-1 units are whole rows (fused finalize possible)
+  unsigned* d_ready = nullptr;       // [nprob][2] fused-finalize ready words (zeroed per run)
   int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
 };
 
@@ -327,6 +333,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   // stage-1 / finalize units of the small jobs (I <= kThinRows) go last: when their
   // fused one-block path runs (k_mse_small_admm), the launches take only the others
   pl.small.clear();
+  pl.rows_aligned = true;
   const long long fin_cap = 1024LL * pl.fin_groups;
   for (int pass = 0; pass < 2; ++pass) {
     for (int i : order) {
@@ -340,15 +347,23 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       d.fin_rows = d.ld <= fin_cap ? (int)(fin_cap / d.ld) : 0;
       for (long long e = 0; e < tot; e += step)
         pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + step), d.H, d.Fp, d.mv.sel});
+      // stage-1 units: whole rows where a row fits (the fused finalize needs them), each
+      // with the job's finalize inputs; `total` is the unit's end
       const long long hu = (long long)kHistElems * pl.hist_nv;
-      for (long long e = 0; e < tot; e += hu) pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, tot});
-      d.mv.nhist = (int)((tot + hu - 1) / hu);
+      const long long hstep = d.ld <= hu ? (hu / d.ld) * d.ld : hu;
+      if (pass == 0 && d.ld > hu) pl.rows_aligned = false;
+      int nh = 0;
+      for (long long e = 0; e < tot; e += hstep, ++nh)
+        pl.hist_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + hstep), d.H, d.Fp, d.mv.sel});
+      d.mv.nhist = nh;
     }
     if (pass == 0) { pl.nfin_big = (int)pl.fin_chunks.size(); pl.nhist_big = (int)pl.hist_chunks.size(); }
   }
   long long small_max = 0;
   for (int i : pl.small) small_max = std::max(small_max, (long long)pl.desc[i].I * pl.desc[i].ld);
   pl.small_groups = small_admm_groups(small_max);
+  pl.d_ready = cv.take<unsigned>(2 * (size_t)nprob);
+  for (int i = 0; i < nprob; ++i) pl.desc[i].mv.ready = pl.d_ready ? pl.d_ready + 2 * i : nullptr;
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
@@ -393,7 +408,7 @@ __global__ void k_export_info(const ProbDesc* __restrict__ d, int n, int32_t* in
     info[4 * i + 0] = d[i].flags[1];
     info[4 * i + 1] = d[i].flags[0];
     info[4 * i + 2] = d[i].flags[2];
-    info[4 * i + 3] = 0;
+    info[4 * i + 3] = d[i].flags[3];   // internal fault (fused-finalize wait timed out)
   }
 }
 
@@ -486,7 +501,7 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
       if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
       if (!groups.empty() && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
       launch_mse_hist3(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, pl.d_rank0,
-                       pl.d_groups, (int)groups.size() / 6, 1, s);
+                       pl.d_groups, (int)groups.size() / 6, 1, false, 0, s);
     } else if (!all) {
       launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, 1, s);
     } else {   // exhaustive: every candidate's canonical SSE over all chunks
@@ -521,6 +536,13 @@ int32_t admmq_set_solve_mode(int32_t mode) {
 }
 
 int32_t admmq_get_solve_mode(void) { return g_solve_mode.load(); }
+
+// diagnostics (not in include/admmq.h): 1 (default) = finalize fused into the search
+// launch where its blocks are all resident, 0 = the separate finalize launch
+int32_t admmq_debug_set_fused_finalize(int32_t enable) {
+  g_fused_finalize = enable != 0;
+  return ADMMQ_OK;
+}
 
 // diagnostics (not in include/admmq.h): workspace bytes of the plan carved against a
 // non-null base (no memory is touched), so a test can check that sizing (null base)
@@ -627,6 +649,12 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   }
   const bool fuse_small = qscheme == kMse && !exhaustive && merged && !pl.small.empty() &&
                           pl.small_groups > 0 && num_attempts <= 1024;
+  // the big jobs' finalize inside the search launch when all its blocks fit at once
+  const int nh_big = fuse_small ? pl.nhist_big : nhist;
+  const bool fuse_fin = g_fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0 &&
+                        nh_big <= hist3_fin_capacity(num_attempts, bits, pl.hist_nv);
+  if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned), s) != hipSuccess)
+    return check_hip("ready reset");
   for (int it = 0; it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
@@ -648,7 +676,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
         if (nh > 0) {
           prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
           launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, nh, num_attempts, bits, slot, pl.d_rank0, pl.d_groups,
-                           ngroups, pl.hist_nv, s);
+                           ngroups, pl.hist_nv, fuse_fin, it, s);
           prof_mark(s);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each
@@ -668,7 +696,8 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
         prof_mark(s);
       }
     }
-    const int nf = fuse_small ? pl.nfin_big : nfin;
+    // fused: every job's finalize ran in the search launch (big jobs) or the small-job kernel
+    const int nf = fuse_fin ? 0 : (fuse_small ? pl.nfin_big : nfin);
     if (nf > 0) {
       prof_class(ADMMQ_PROF_FINALIZE); prof_mark(s);
       launch_finalize_admm(pl.d_desc, pl.d_fin, nf, pl.fin_groups, num_attempts, bits, qscheme, slot, it, s);

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   __shared__ double red[16];
   __shared__ int last;
   // this thread's 4 elements: issued first, so the load overlaps the table setup
-  const long long total = (long long)v.rows * v.ld;
+  const long long total = ck.total;   // the unit's end (ADMM units are whole rows; standalone: the job's end)
   float4 x4v[NV];   // NV float4 per thread: start + 4 tid + 4096 g
 #pragma unroll
   for (int g = 0; g < NV; ++g) {
@@ -964,11 +964,24 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
   t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
 }
 
-template <int QMAX, int NV>
-__global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __restrict__ d, const QJob* __restrict__ qj,
-                                                      const Chunk* __restrict__ chunks, int ncand, int slot,
-                                                      const unsigned short* __restrict__ rank0,
-                                                      const unsigned short* __restrict__ groups, int ngroups) {
+// FIN (ADMM jobs only): the search launch also runs the finalize step (k_finalize_admm's
+// projection + dual update + next right-hand side) on the block's own elements, which
+// it already holds: units are whole rows, every block of the launch is resident at once
+// (the host checks the occupancy), and after its ticket each block waits for its job's
+// selection. The last block of a job publishes the selection record with write-through
+// (sc1) stores, then the job's ready word = iter + 1; the others poll that word (one
+// wave, relaxed agent-scope loads with s_sleep) and read the record with sc1 loads. The
+// wait is bounded: past ~10 ms the block stops waiting, sets flags[3] (reported as an
+// internal fault by admmq_admm_run's info) and finishes, so a broken residency
+// assumption cannot hang the GPU. Saves the finalize launch, its dependent parameter
+// chain and its re-read of H_T and U.
+constexpr unsigned kFinWaitPolls = 1u << 17;
+
+template <int QMAX, int NV, bool FIN>
+__global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
+    const ProbDesc* __restrict__ d, const QJob* __restrict__ qj, const Chunk* __restrict__ chunks, int ncand, int slot,
+    const unsigned short* __restrict__ rank0, const unsigned short* __restrict__ groups, int ngroups, int bits,
+    int iter) {
   const unsigned long long T0 = ADMMQ_NOW();
   const Chunk ck = chunks[blockIdx.x];
   // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
@@ -980,7 +993,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   H3Pre pre;
   h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kH3Threads);
   asm volatile("" ::: "memory");   // issue order: the loads above before the element loads
-  float4 x4[2 * NV], u4[2 * NV];
+  float4 x4[2 * NV], u4[2 * NV], h4[FIN ? 2 * NV : 1], f4[FIN ? 2 * NV : 1];
 #pragma unroll
   for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
     const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
@@ -996,12 +1009,33 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   const MseView& v = mview(d, qj, ck.job);
   if (stopped) return;
   int* sel = v.sel + (size_t)slot * (2 + kMaxSel);
-  if (mse_degenerate(mx)) {     // finalize emits NaN for degenerate mx
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ double red[8];
+  __shared__ unsigned long long wtot[8], wtot2[8];
+  __shared__ unsigned wtot32[8], wtot32b[8];
+  __shared__ int last;
+  __shared__ int lsel[2 + kMaxSel];
+  const int n = ncand;
+  // the finalize step's other inputs (current H, padded F): issued after the search
+  // (FIN: before the wait for the selection), so they hold no registers during the search
+  auto load_hf = [&]() {
+#pragma unroll
+    for (int hh = 0; hh < 2 * NV; ++hh) {
+      const long long ec = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+      h4[hh] = gld4(ck.H + (ec < total ? ec : 0));
+      f4[hh] = gld4(ck.F + (ec < total ? ec : 0));
+    }
+  };
+  if (mse_degenerate(mx)) {     // the projection emits NaN for degenerate mx (no search)
     if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
+    if constexpr (FIN) {
+      load_hf();
+      const ProbDesc& p = d[ck.job];
+      admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qparams_mse(bits, __builtin_nanf("")),
+                                              slot, iter, blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+    }
     return;
   }
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int n = ncand;
   const int M = QMAX * n;
   const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
   unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
@@ -1012,25 +1046,20 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
   float* tsort = thr + M;                                                    // M
   unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
   unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
-  __shared__ double red[8];
-  __shared__ unsigned long long wtot[8], wtot2[8];
-  __shared__ unsigned wtot32[8], wtot32b[8];
-  __shared__ int last;
   const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, rank0 + kMaxMerged, sumA, sumN, cntA, cntN, thr, tsort,
                                    rnk, cell, kH3Threads);
   const unsigned long long T1 = ADMMQ_NOW();
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
-#pragma unroll
-  for (int hh = 0; hh < 2 * NV; ++hh) {   // X - U (ADMM: H_T - U); zero past the end
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
-    if (ck.U) x4[hh] = sub4(x4[hh], u4[hh]);
-    if (e >= total) x4[hh] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   double s2 = 0.0;
 #pragma unroll
-  for (int hb = 0; hb < 2 * NV; hb += 2) {
-    const float xs[8] = {x4[hb].x, x4[hb].y, x4[hb].z, x4[hb].w, x4[hb + 1].x, x4[hb + 1].y, x4[hb + 1].z, x4[hb + 1].w};
+  for (int hb = 0; hb < 2 * NV; hb += 2) {   // X - U (ADMM: H_T - U); zero past the end
+    float4 xa = x4[hb], xb = x4[hb + 1];
+    if (ck.U) { xa = sub4(xa, u4[hb]); xb = sub4(xb, u4[hb + 1]); }
+    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hb;
+    if (e >= total) xa = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e + 2048 >= total) xb = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
     h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
@@ -1072,52 +1101,94 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(const ProbDesc* __r
       g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4; g_hist_trace[blockIdx.x][5] = 0;
     }
   };
-  if (!last) { trace(T3); return; }
-  // every byte handed over by the other blocks (h1/h2 replicas, s2) was written by
-  // memory-side atomics drained before the ticket and is read below by agent-scope
-  // (sc1) atomic loads only, so no L1 invalidate is needed (cdna_hip_programming.md
-  // Guideline 16, sc1 consumer); the wavefront fence only keeps the loads after the ticket
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
-  const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
-  __shared__ int lsel[2 + kMaxSel];
-  if (n <= (int)blockDim.x) {
-    const int c = threadIdx.x;
-    unsigned long long t1 = 0ull, t2 = 0ull;
-    if (c < n) {
+  if (last) {
+    // every byte handed over by the other blocks (h1/h2 replicas, s2) was written by
+    // memory-side atomics drained before the ticket and is read below by agent-scope
+    // (sc1) atomic loads only, so no L1 invalidate is needed (cdna_hip_programming.md
+    // Guideline 16, sc1 consumer); the wavefront fence only keeps the loads after the ticket
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
+    const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
+    if (n <= (int)blockDim.x) {
+      const int c = threadIdx.x;
+      unsigned long long t1 = 0ull, t2 = 0ull;
+      if (c < n) {
 #pragma unroll
-      for (int r = 0; r < kHistRep; ++r) {
-        t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int r = 0; r < kHistRep; ++r) {
+          t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
+      const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+      select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
+    } else {
+      unsigned long long* T1v = sumA;                 // reuse LDS: n each
+      unsigned long long* T2v = sumN;
+      for (int c = threadIdx.x; c < n; c += blockDim.x) {
+        unsigned long long t1 = 0ull, t2 = 0ull;
+#pragma unroll
+        for (int r = 0; r < kHistRep; ++r) {
+          t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        T1v[c] = t1; T2v[c] = t2;
+      }
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        select_wave2(v, sel, lsel, T1v, T2v, S2, mx, n, QMAX);
+      }
+      __syncthreads();
     }
-    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
     sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
     trace(ADMMQ_NOW());
-    return;
-  }
-  unsigned long long* T1v = sumA;                 // reuse LDS: n each
-  unsigned long long* T2v = sumN;
-  for (int c = threadIdx.x; c < n; c += blockDim.x) {
-    unsigned long long t1 = 0ull, t2 = 0ull;
-#pragma unroll
-    for (int r = 0; r < kHistRep; ++r) {
-      t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (FIN) {   // publish: the record write-through, drained, then the ready word
+      const int nrec = 2 + min(lsel[0], kMaxSel);
+      for (int j = threadIdx.x; j < nrec; j += blockDim.x)
+        __hip_atomic_store(sel + j, lsel[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_store(v.ready + slot, (unsigned)(iter + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    T1v[c] = t1; T2v[c] = t2;
+  } else {
+    trace(T3);
   }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    select_wave2(v, sel, lsel, T1v, T2v, S2, mx, n, QMAX);
+  if constexpr (FIN) {
+    const ProbDesc& p = d[ck.job];
+    load_hf();
+    if (!last) {   // wait for the job's selection (bounded)
+      if (threadIdx.x == 0) {
+        unsigned polls = 0;
+        while (__hip_atomic_load(v.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)(iter + 1)) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++polls == kFinWaitPolls) {
+            __hip_atomic_store(p.flags + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        lsel[0] = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lsel[2] = __hip_atomic_load(sel + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
+    QParams qp;
+    if (lsel[0] == 1) {
+      qp = qparams_mse(bits, cand_t(mx, lsel[2], n));
+    } else {   // |S| > 1: the canonical SSEs decide (written by the last block's atomics)
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      qp = block_qparams(kMse, bits, v, slot, n, 0, 0.f, 0.f);
+    }
+    __syncthreads();   // the search tables' LDS is reused as rmax
+    admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
+                                            blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
   }
-  __syncthreads();
-  sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
-  trace(ADMMQ_NOW());
 }
 
 // Small ADMM jobs (thin factors, I <= kThinRows: the 9-row spatial mode of a 3x3 conv,
@@ -1408,13 +1479,21 @@ bool merged_ok(int ncand, int bits) {
   return ncand >= 2 && ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist3_lds_bytes(ncand, bits) <= 150 * 1024;
 }
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
-                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, hipStream_t s) {
+                      const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
+                      hipStream_t s) {
   if (nchunks <= 0) return;
   const size_t lds = hist3_lds_bytes(ncand, bits);
-#define ADMMQ_H3(Q, V)                                                                                        \
-  hipLaunchKernelGGL((k_mse_hist3<Q, V>), dim3(nchunks), dim3(kH3Threads), lds, s, d, q, chunks, ncand, slot, rank0, \
-                     groups, ngroups)
-#define ADMMQ_H3N(Q) if (nv == 2) ADMMQ_H3(Q, 2); else ADMMQ_H3(Q, 1)
+#define ADMMQ_H3(Q, V, F)                                                                                        \
+  hipLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, d, q, chunks, ncand, slot, \
+                     rank0, groups, ngroups, bits, iter)
+#define ADMMQ_H3N(Q)                               \
+  if (fin) {                                       \
+    if (nv == 2) ADMMQ_H3(Q, 2, true);             \
+    else ADMMQ_H3(Q, 1, true);                     \
+  } else {                                         \
+    if (nv == 2) ADMMQ_H3(Q, 2, false);            \
+    else ADMMQ_H3(Q, 1, false);                    \
+  }
   switch (bits) {
     case 1: ADMMQ_H3N(1); break;
     case 2: ADMMQ_H3N(2); break;
@@ -1424,6 +1503,33 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
   }
 #undef ADMMQ_H3N
 #undef ADMMQ_H3
+}
+
+// Resident blocks of the fused (FIN) search kernel on this device (all of a launch's
+// blocks must be resident at once for its in-kernel wait): occupancy x CUs.
+int hist3_fin_capacity(int ncand, int bits, int nv) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      cus = 0;
+  }
+  const size_t lds = hist3_lds_bytes(ncand, bits);
+  int per = 0;
+  hipError_t e = hipErrorInvalidValue;
+#define ADMMQ_OCC(Q) \
+  e = nv == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 2, true>, kH3Threads, lds) \
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 1, true>, kH3Threads, lds)
+  switch (bits) {
+    case 1: ADMMQ_OCC(1); break;
+    case 2: ADMMQ_OCC(2); break;
+    case 3: ADMMQ_OCC(4); break;
+    case 4: ADMMQ_OCC(8); break;
+    default: ADMMQ_OCC(16); break;
+  }
+#undef ADMMQ_OCC
+  return e == hipSuccess ? per * cus : 0;
 }
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {
   if (njobs > 0) hipLaunchKernelGGL(k_mse_select_all, dim3(njobs), dim3(64), 0, s, d, q, ncand, slot);

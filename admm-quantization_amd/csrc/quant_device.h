@@ -311,4 +311,112 @@ __device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 
   *reinterpret_cast<h4*>(b + 32) = lo;
 }
 
+// ---------------------------------------------------------------------------
+// ADMM finalize of one unit of whole rows [start, end) of problem p (source/admm.py:58-63):
+// H = Q(X) with X = H_T - U re-formed here, U += H - H_T, the next right-hand side
+// P = F + rho (H + U) (split form: fp16 planes with the row's exponent), and the
+// residual sums of the r / s stop test into replica `rep`. The float4 group g of thread
+// t is element start + 4 t + 4 NT g; t4 = H_T, u4 = U, h4 = H (current), f4 = F.
+// rmax: LDS of >= the unit's rows. Every thread of the block calls it. Used by
+// k_finalize_admm and by the search kernel's fused finalize (k_mse_hist3<.., true>).
+template <int NT, int NG>
+__device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long start, long long end,
+                                                    const float4* t4, const float4* u4, const float4* h4,
+                                                    const float4* f4, const QParams& qp, int slot, int iter, int rep,
+                                                    unsigned* rmax) {
+  __shared__ double red[NT / 64][4];
+  const float rho = p.rho[0];
+  const bool split = p.split != 0;
+  const int row0 = (int)(start / p.ld);
+  if (split) {
+    const int nrows = (int)((end - start + p.ld - 1) / p.ld);
+    for (int r = threadIdx.x; r < nrows; r += NT) rmax[r] = 0u;
+    __syncthreads();
+  }
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  float4 p4[NG];
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const long long e = start + 4LL * threadIdx.x + 4LL * NT * g;
+    p4[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool in = e < end;
+    const int row = in ? (int)(e / p.ld) : 0x7FFFFFFF;
+    if (in) {
+      const int c0 = (int)(e - (long long)row * p.ld);
+      const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
+      const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
+      const float xs[4] = {ts[0] - us[0], ts[1] - us[1], ts[2] - us[2], ts[3] - us[3]};   // H_T - U
+      const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
+      float ho[4], uo[4], po[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (c0 + k < p.R) {
+          const float hn = apply_quant(xs[k], qp);          // H = quantize(H_T - U)
+          const float dh = hn - ts[k];
+          const float un = us[k] + dh;                      // U += H - H_T
+          ho[k] = hn; uo[k] = un;
+          po[k] = fs[k] + rho * (hn + un);                  // next rhs F + rho(H+U)
+          const float dp = hn - hs[k];
+          s1 += (double)(dh * dh); s2 += (double)(hn * hn);
+          s3 += (double)(dp * dp); s4 += (double)(un * un);
+        } else {
+          ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
+        }
+      }
+      *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
+      *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
+      p4[g] = make_float4(po[0], po[1], po[2], po[3]);
+      if (!split) *reinterpret_cast<float4*>(p.P + e) = p4[g];
+    }
+    if (split) {   // uniform: row max of |next P| (a float4 never straddles a row, ld % 32 == 0)
+      // segmented max over the wave's lanes of one row (rows are contiguous lane ranges),
+      // then one LDS atomic per (wave, row) instead of one per lane
+      unsigned mv = __float_as_uint(fmaxf(fmaxf(fabsf(p4[g].x), fabsf(p4[g].y)), fmaxf(fabsf(p4[g].z), fabsf(p4[g].w))));
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned o = (unsigned)__shfl_down((int)mv, off);
+        const int ro = __shfl_down(row, off);
+        if (lane + off < 64 && ro == row) mv = max(mv, o);
+      }
+      const int rp = __shfl_up(row, 1);
+      if (in && (lane == 0 || rp != row)) atomicMax(&rmax[row - row0], mv);
+    }
+  }
+  if (split) {
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const long long e = start + 4LL * threadIdx.x + 4LL * NT * g;
+      if (e >= end) continue;
+      const int row = (int)(e / p.ld);
+      const int c0 = (int)(e - (long long)row * p.ld);
+      const int ex = split_exponent(__uint_as_float(rmax[row - row0]));
+      split_store4(p.P2 + (size_t)row * 2 * p.ld, c0, p4[g], ex);
+      if (c0 == 0) p.eP[row] = ex;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off);
+    s3 += __shfl_xor(s3, off); s4 += __shfl_xor(s4, off);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[w][0] = s1; red[w][1] = s2; red[w][2] = s3; red[w][3] = s4; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) v += red[k][threadIdx.x];
+    atomicAdd(&p.res[4 * (kResRep * slot + rep) + threadIdx.x], v);
+  }
+  if (start == 0 && threadIdx.x == 0) {
+    p.flags[1] = iter + 1;
+    unsigned* st = p.mv.stat + 4 * (slot ^ 1);
+    st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
+    double* rs = p.res + 4 * kResRep * (slot ^ 1);
+    for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
+  }
+}
+
 }  // namespace admmq

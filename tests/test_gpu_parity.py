@@ -379,3 +379,30 @@ def test_stage1_host_cell_bound(torch_dev, n, bits):
         assert lib.admmq_debug_check_cells(n, bits, seed, 2048, ctypes.byref(dev)) == 0
     print(f"n={n} bits={bits}: max deviation {dev.value * 1e-6:.2e} cells")
     assert dev.value * 1e-6 < 0.05
+
+
+@pytest.mark.parametrize("eps", [0.0, 1e-3])
+def test_fused_finalize_equals_separate(torch_dev, eps):
+    """The big jobs' finalize inside the search launch (k_mse_hist3<.., true>, in-kernel
+    wait for the job's selection) gives the same bits as the separate k_finalize_admm
+    launch: H, U and the iteration counts (eps = 1e-3 exercises the early exit), over
+    all 16 resnet18 factors of mode 0 plus the 9-row mode-2 factors; no internal fault."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    probs_np = [_layer_problem(l, m) for l, m in [("layer1.0.conv1", 0), ("layer2.1.conv1", 0),
+                                                 ("layer3.1.conv2", 1), ("layer4.1.conv2", 0),
+                                                 ("layer4.0.conv1", 1), ("layer1.1.conv2", 2)]]
+
+    def run(fused):
+        ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+              for H, F, G in probs_np]
+        with _lib.fused_finalize(fused):
+            Hs, info = admm_iteration_batched(ps, 12, eps, 4, MSE, return_info=True)
+        return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
+
+    a, ia = run(True)
+    b, ib = run(False)
+    assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
+    assert np.array_equal(ia, ib)
+    for (ha, ua), (hb, ub) in zip(a, b):
+        assert _bits_equal(ha, hb) and _bits_equal(ua, ub)

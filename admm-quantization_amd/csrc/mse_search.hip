@@ -1186,8 +1186,15 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
       qp = block_qparams(kMse, bits, v, slot, n, 0, 0.f, 0.f);
     }
     __syncthreads();   // the search tables' LDS is reused as rmax
+    if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) g_hist_trace[blockIdx.x][5] = ADMMQ_NOW();
     admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
                                             blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+    if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
+      // columns 4, 5: {wait for the selection done, finalize done} (the search ended at 3 / 4)
+      const unsigned long long tw = g_hist_trace[blockIdx.x][5];
+      g_hist_trace[blockIdx.x][4] = tw;
+      g_hist_trace[blockIdx.x][5] = ADMMQ_NOW();
+    }
   }
 }
 

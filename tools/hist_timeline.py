@@ -46,8 +46,14 @@ for b in range(got):
 t0 = min(r[0] for r in rows)
 t1 = max(r[4] for r in rows)
 print(f"blocks {len(rows)}  span {(t1 - t0) / 100:.2f} us")
-for name, j0, j1 in (("setup/tables", 0, 1), ("elements", 1, 2), ("scan+flush+ticket", 2, 3), ("select+stage2", 3, 4),
-                     ("total", 0, 4)):
+fused = any(r[5] for r in rows)
+phases = (("setup/tables", 0, 1), ("elements", 1, 2), ("scan+flush+ticket", 2, 3), ("select+stage2", 3, 4), ("total", 0, 4))
+if fused:   # fused finalize: column 4 = selection received, 5 = finalize done
+    phases = (("setup/tables", 0, 1), ("elements", 1, 2), ("scan+flush+ticket", 2, 3),
+              ("ticket->selection", 3, 4), ("finalize", 4, 5), ("total", 0, 5))
+    t1 = max(r[5] for r in rows)
+    print(f"  fused finalize: span to last finalize {(t1 - t0) / 100:.2f} us")
+for name, j0, j1 in phases:
     d = [(r[j1] - r[j0]) / 100 for r in rows]
     print(f"  {name:13s} avg {sum(d)/len(d):7.2f}  max {max(d):7.2f} us")
 starts = sorted((r[0] - t0) / 100 for r in rows)

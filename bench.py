@@ -256,31 +256,40 @@ def load_traffic(model, split):
 
 def cpu_baseline(work, max_iter_admm, sample_iters=20):
     """torch-CPU port of the reference step (oracle/torch_port.py) on a bounded sample:
-    every (layer, mode) of the workload, setup + `sample_iters` inner iterations timed,
-    extrapolated linearly to max_iter_admm-1 iterations (per-iteration cost is constant
-    with eps=0)."""
+    every DISTINCT (layer shape, rank, mode) problem of the workload runs its setup plus
+    `sample_iters` inner iterations on the host cores; the per-iteration cost (constant
+    with eps=0) is extrapolated to max_iter_admm-1 iterations and weighted by how many
+    (layer, mode) problems of the workload share that shape."""
     from oracle import torch_port
+    classes = {}
+    for (s, W, R, init) in work:
+        for m in range(len(s.shape)):
+            key = (tuple(s.shape), R, m)
+            if key not in classes:
+                classes[key] = [0, W, init]
+            classes[key][0] += 1
     total = 0.0
     n_fi = 0
     wall = time.time()
-    for (s, W, R, init) in work:
+    for (shape, R, m), (count, W, init) in classes.items():
         Wc = W.cpu()
         fs = [f.cpu() for f in init]
-        for m in range(len(s.shape)):
-            G, F = torch_port.gram_mttkrp(Wc, fs, m)
-            t0 = time.perf_counter()
-            torch_port.admm_iteration(fs[m], torch.zeros_like(fs[m]), F, G, 1, 0.0, 4)
-            t1 = time.perf_counter()
-            torch_port.admm_iteration(fs[m], torch.zeros_like(fs[m]), F, G, 1 + sample_iters, 0.0, 4)
-            t2 = time.perf_counter()
-            setup = t1 - t0
-            per_iter = max((t2 - t1) - setup, 0.0) / sample_iters
-            total += setup + per_iter * (max_iter_admm - 1)
-            n_fi += max_iter_admm - 1
+        G, F = torch_port.gram_mttkrp(Wc, fs, m)
+        t0 = time.perf_counter()
+        torch_port.admm_iteration(fs[m], torch.zeros_like(fs[m]), F, G, 1, 0.0, 4)
+        t1 = time.perf_counter()
+        torch_port.admm_iteration(fs[m], torch.zeros_like(fs[m]), F, G, 1 + sample_iters, 0.0, 4)
+        t2 = time.perf_counter()
+        setup = t1 - t0
+        per_iter = max((t2 - t1) - setup, 0.0) / sample_iters
+        total += count * (setup + per_iter * (max_iter_admm - 1))
+        n_fi += count * (max_iter_admm - 1)
+    nprob = sum(c[0] for c in classes.values())
     return {"value": n_fi / total, "unit": "factor-iterations/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{len(work)} layers x modes: setup + {sample_iters} inner iterations each timed on host cores "
-                      f"(torch-CPU port of source/admm.py + quantization.py, oracle/torch_port.py), extrapolated "
-                      f"to {max_iter_admm - 1} iterations; {time.time() - wall:.1f}s of CPU work"}
+            "sample": f"{len(classes)} distinct (shape, rank, mode) problems of the workload's {nprob}: setup + "
+                      f"{sample_iters} inner iterations each timed on host cores (torch-CPU port of source/admm.py + "
+                      f"quantization.py, oracle/torch_port.py), extrapolated to {max_iter_admm - 1} iterations and "
+                      f"weighted by multiplicity; {time.time() - wall:.1f}s of CPU work"}
 
 
 def parity_check(device):

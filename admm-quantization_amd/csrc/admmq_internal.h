@@ -38,6 +38,7 @@ constexpr int kResRep = 8;         // replicas of the per-problem residual sums 
 constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU split-K solve
 constexpr int kThinCols = 256;     // ... columns per unit (64 lanes x float4)
 constexpr int kThinK = 128;        // ... reduction rows per unit (4 waves x 32)
+constexpr long long kWideMinTiles = 4 * 768;   // 64x64 tiles of a launch from which I > 64 factors take 128x64 tiles
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in
@@ -178,8 +179,8 @@ void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
                       int ncand, hipStream_t s);
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
-                 int iter, float eps, int ncand, hipStream_t s);
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
+                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,

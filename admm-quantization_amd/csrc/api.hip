@@ -165,7 +165,8 @@ struct AdmmPlan {
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
-  int ntiles_big = 0, ntiles_small = 0;
+  int ntiles_wide = 0, ntiles_big = 0, ntiles_small = 0;   // 128x64, 64x64, 32x64 tiles (in that order)
+  bool wide = false;                                       // I > 64 factors take 128x64 tiles (k_gemm<4, ..>)
   int fin_groups = 1;             // float4 groups per thread of the finalize units
   int hist_nv = 1;
   std::vector<int> small;         // jobs with I <= kThinRows (one-block fused search + finalize)
@@ -234,6 +235,16 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i = 0; i < nprob; ++i)
     if (probs[i].I > 0 && probs[i].I <= kThinRows) pl.thin_nr = std::max(pl.thin_nr, probs[i].I);
   pl.split = g_solve_mode.load() == kSolveSplit;
+  // Wide tiles when the 64x64 tiles would take many rounds of the resident slots
+  // (256 CUs x 3): then a CU's bytes per MAC matter more than the number of tiles, and
+  // 128x64 tiles read 3/4 of the operand bytes per MAC (the Llama shapes of C5). The
+  // element results do not depend on the tile shape (same K order per element).
+  {
+    long long t64 = 0;
+    for (int i = 0; i < nprob; ++i)
+      if (probs[i].I > 32) t64 += (long long)((probs[i].I + 63) / 64) * ((rup(std::max(probs[i].R, 1), 32) + 63) / 64);
+    pl.wide = t64 >= kWideMinTiles;
+  }
   for (int i = 0; i < nprob; ++i)   // the split finalize needs whole rows in one unit
     if (probs[i].I > kThinRows && rup(std::max(probs[i].R, 1), 32) > 8192) pl.split = false;
   for (int i = 0; i < nprob; ++i) {
@@ -246,7 +257,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, 64);
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? 128 : 64);
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -286,9 +297,19 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  std::vector<GemmTile> wide;
+  for (int i : order) {   // 128 x 64 tiles (pl.wide, I > 64)
+    const ProbDesc& d = pl.desc[i];
+    if (!(pl.wide && d.I > 64)) continue;
+    const int TM = d.Ip / 128, TN = (d.ld + 63) / 64;
+    for (int g0 = 0; g0 < TN; g0 += 8)
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
+          wide.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+  }
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
-    if (d.I <= kThinRows || d.Ip == 32) continue;   // thin: k_gemm_thin units below; 32-row tiles after
+    if (d.I <= kThinRows || d.Ip == 32 || (pl.wide && d.I > 64)) continue;   // thin / 32-row / wide: elsewhere
     const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
     for (int g0 = 0; g0 < TN; g0 += 8)
       for (int tm = 0; tm < TM; ++tm)
@@ -305,7 +326,9 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   }
   pl.ntiles_big = (int)pl.tiles.size();
   pl.ntiles_small = (int)small.size();
+  pl.ntiles_wide = (int)wide.size();
   pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
+  pl.tiles.insert(pl.tiles.begin(), wide.begin(), wide.end());
   // thin units, most reduction blocks first; counters: one per (problem, column block)
   pl.thin.clear();
   pl.ntcnt = 0;
@@ -659,9 +682,10 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
-    if (pl.ntiles_small + pl.ntiles_big > 0) {
+    if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0) {
       prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
-      launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps, num_attempts, s);
+      launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
+                  num_attempts, s);
       prof_mark(s);
     }
     if (!pl.thin.empty()) {

@@ -93,7 +93,7 @@ __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16
 // One workgroup per tile (the grid is the tile list, longest K first, CU-balanced by the
 // planner). SPLIT selects the operand form (see the file header).
 template <int WM, int KS, int NS, bool SPLIT>
-__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? 3 : 1))) void k_gemm(
+__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? (WM == 4 ? 4 : 3) : 1))) void k_gemm(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
   constexpr int NSUB = 2 * WM;                 // 32 x 32 sub-tiles per workgroup
@@ -136,10 +136,13 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   // the epilogue's U entries (X = H_T - U) and, split form, the row / column exponents:
   // loaded before the first stages so their latency is spent under the K-loop (vector
   // loads complete in issue order: the stage waits below then also cover these)
+  // (wide tiles, WM = 4: loaded in the epilogue instead - those launches run many rounds
+  // of tiles, so other workgroups cover the latency, and the registers stay free)
+  constexpr bool PRE = WM < 4;
   float upre[16];
   int epre[16];
   int ecol = 0;
-  {
+  auto load_epi = [&]() {
     const int col = col0 + 32 * wn + i;
     const int colc = col < ld ? col : 0;
 #pragma unroll
@@ -149,7 +152,8 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
       if (SPLIT) epre[r] = *(__attribute__((address_space(1))) const int*)(tl.eP + row);
     }
     if (SPLIT) ecol = *(__attribute__((address_space(1))) const int*)(tl.eM + colc);
-  }
+  };
+  if constexpr (PRE) load_epi();
   // per-lane global source of each of this wave's glds pieces (K-step 0)
   const float* src[GPW];
 #pragma unroll
@@ -257,6 +261,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
 
   // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   if (ks == 0) {
+    if constexpr (!PRE) load_epi();
     const int col = col0 + 32 * wn + i;
     unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
     if (col < ld) {
@@ -536,24 +541,23 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
   if (nprob > 0 && maxrows > 0) hipLaunchKernelGGL(k_split_rows, dim3(maxrows, nprob), dim3(256), 0, s, d, which);
 }
 
-void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_small, int ntiles_big, bool split, int slot,
-                 int iter, float eps, int ncand, hipStream_t s) {
-  // tiles[0 .. ntiles_big) are 64x64 (WM = 2, one wave per 32x32 sub-tile, 3-deep ring),
-  // then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors, 2 waves per sub-tile
-  // splitting each K-step, 4-deep ring)
-  if (ntiles_big > 0) {
-    if (split)
-      hipLaunchKernelGGL((k_gemm<2, 1, 3, true>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
-    else
-      hipLaunchKernelGGL((k_gemm<2, 1, 3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
-  }
-  if (ntiles_small > 0) {
-    const GemmTile* t = tiles + ntiles_big;
-    if (split)
-      hipLaunchKernelGGL((k_gemm<1, 2, 4, true>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
-    else
-      hipLaunchKernelGGL((k_gemm<1, 2, 4, false>), dim3(ntiles_small), dim3(256), 0, s, d, t, slot, iter, eps, ncand);
-  }
+void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
+                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s) {
+  // tiles[0 .. ntiles_wide) are 128x64 (WM = 4: eight waves, one per 32x32 sub-tile, the
+  // launches with many rounds of tiles), then ntiles_big 64x64 tiles (WM = 2, four
+  // waves, 3-deep ring), then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors,
+  // 2 waves per sub-tile splitting each K-step, 4-deep ring)
+#define ADMMQ_GEMM(WM, KS, NS, N, T)                                                                                 \
+  do {                                                                                                               \
+    if (split)                                                                                                       \
+      hipLaunchKernelGGL((k_gemm<WM, KS, NS, true>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_gemm<WM, KS, NS, false>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
+  } while (0)
+  if (ntiles_wide > 0) ADMMQ_GEMM(4, 1, 3, ntiles_wide, tiles);
+  if (ntiles_big > 0) ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
+  if (ntiles_small > 0) ADMMQ_GEMM(1, 2, 4, ntiles_small, tiles + ntiles_wide + ntiles_big);
+#undef ADMMQ_GEMM
 }
 
 void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,

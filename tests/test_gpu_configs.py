@@ -160,3 +160,31 @@ def test_c5_llama_shapes(torch_dev, I, J, R, solve):
     probs = [("llama", A.cpu().numpy(), F.cpu().numpy(), G.cpu().numpy())]
     worst = _check_step(torch, dev, probs, solve, _fp64_ht)
     print(f"C5 ({I},{J}) R={R} {solve}: H_T rel vs fp64 {worst:.2e}")
+
+
+def test_wide_tiles_equal_64x64(torch_dev):
+    """The 128x64 tiles (a launch with >= kWideMinTiles 64x64 tiles, e.g. the Llama MLP
+    factor) compute each element with the same K order as the 64x64 tiles: a (512, 1141)
+    factor solved beside an (11008, 1492) one (wide tiles) equals the same factor solved
+    alone (64x64 tiles) bit for bit, over 3 inner iterations, in both solve forms."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    from admmq._lib import solve_mode
+    g = torch.Generator().manual_seed(11)
+
+    def prob(I, R):
+        B = torch.randn(R, 2 * R, generator=g) / (2 * R) ** 0.5
+        return (torch.randn(I, R, generator=g) * 0.1, torch.randn(I, R, generator=g), B @ B.T + 0.5 * torch.eye(R))
+
+    small, big = prob(512, 1141), prob(11008, 1492)
+
+    def run(ps):
+        args = [(H.to(dev), torch.zeros(H.shape, device=dev), F.to(dev), G.to(dev)) for H, F, G in ps]
+        Hs = admm_iteration_batched(args, 4, 0.0, 4, MSE)
+        return Hs[0].cpu(), args[0][1].cpu()
+
+    for form in ("split", "fp32"):
+        with solve_mode(form):
+            h1, u1 = run([small, big])
+            h2, u2 = run([small])
+        assert torch.equal(h1, h2) and torch.equal(u1, u2), form

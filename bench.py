@@ -143,7 +143,8 @@ SPLIT_PRODUCTS = 3             # split-fp16 solve: Ph Mh + Ph Ml + Pl Mh per sol
 # problem. Bytes are the compulsory HBM bytes of DESIGN.md §4 (fp32 = 4 B; the split
 # planes are 2 x 2 B = 4 B per element too):
 #   gemm / gemm_thin  H_T = P M: 2 I R^2 flops; read P, U, M, write H_T: 4 (3 I R + R^2) B
-#   search            stage 1 + selection + stage 2 over X = H_T - U: read H_T, U: 8 I R B
+#   search            stage 1 + selection + stage 2 over X = H_T - U: read H_T, U: 8 I R B;
+#                     with the finalize fused into the launch (k_mse_hist3<.., true>): 28 I R B
 #                     (SURVEY §8(d) counts the reference's exhaustive sweep, 8 x 200 flops
 #                     per element; reported beside the byte roofline as `valu_equiv`)
 #   small             search + finalize of the I <= 16 factors in one block: 8 I R + 28 I R B
@@ -161,7 +162,7 @@ def mode_problems(work):
     return [[(s.shape[m], R) for (s, _, R, _) in work if m < len(s.shape)] for m in range(nm)]
 
 
-def class_work(work, num_attempts=200, split=True):
+def class_work(work, num_attempts=200, split=True, fused=False):
     """Per launch class: (flops, bytes, valu_equiv_flops) of ONE launch, averaged over the
     modes whose calls issue it. The HIP-event sampling times one iteration in N of every
     mode call, so each issuing mode weighs equally in the measured average duration."""
@@ -177,8 +178,8 @@ def class_work(work, num_attempts=200, split=True):
             fl = sum(2.0 * i * r * r for (i, r) in sel) if cls.startswith("gemm") else 0.0
             if cls.startswith("gemm"):
                 by = sum(4.0 * (3 * i * r + r * r) for (i, r) in sel)
-            elif cls == "search":
-                by = sum(8.0 * i * r for (i, r) in sel)
+            elif cls == "search":   # fused: + the finalize step's H, F reads and H, U, P writes
+                by = sum((28.0 if fused else 8.0) * i * r for (i, r) in sel)
             elif cls == "small":
                 by = sum(36.0 * i * r for (i, r) in sel)
             else:
@@ -402,9 +403,12 @@ def main():
             ms, cnt = kern["ms"], kern["launches"]
             avg_us = {c: 1e3 * ms[i] / cnt[i] for i, c in enumerate(PROF_CLASSES) if cnt[i]}
             traffic = load_traffic(a.model, split)
-            cw = class_work(work, split=split)
+            fused = "search" in avg_us and "finalize" not in avg_us   # the big jobs' finalize ran in the search launch
+            cw = class_work(work, split=split, fused=fused)
             rf = {c: kernel_roofline(c, cw[c], avg_us[c], cnt[i], split, traffic)
                   for i, c in enumerate(PROF_CLASSES[:5]) if c in cw and c in avg_us}
+            if fused and "search" in rf:
+                rf["search"]["kernel"] = "k_mse_hist3 (two-stage MSE search + fused finalize)"
             # per step: each class launches once per inner iteration of every mode that issues it
             n_issuing = {c: sum(1 for probs in mode_problems(work)
                                 if any((i <= THIN_ROWS) == (c in ("gemm_thin", "small")) for (i, _) in probs))

@@ -373,14 +373,20 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
       // segmented max over the wave's lanes of one row (rows are contiguous lane ranges),
       // then one LDS atomic per (wave, row) instead of one per lane
       unsigned mv = __float_as_uint(fmaxf(fmaxf(fabsf(p4[g].x), fabsf(p4[g].y)), fmaxf(fabsf(p4[g].z), fabsf(p4[g].w))));
+      const int rfirst = __builtin_amdgcn_readfirstlane(row), rlast = __builtin_amdgcn_readlane(row, 63);
+      if (rfirst == rlast) {   // the whole wave in one row (rows of >= 256 elements): a plain wave max
+        mv = wave_max_u32(mv);
+        if (lane == 0 && in) atomicMax(&rmax[row - row0], mv);
+      } else {
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const unsigned o = (unsigned)__shfl_down((int)mv, off);
-        const int ro = __shfl_down(row, off);
-        if (lane + off < 64 && ro == row) mv = max(mv, o);
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned o = (unsigned)__shfl_down((int)mv, off);
+          const int ro = __shfl_down(row, off);
+          if (lane + off < 64 && ro == row) mv = max(mv, o);
+        }
+        const int rp = __shfl_up(row, 1);
+        if (in && (lane == 0 || rp != row)) atomicMax(&rmax[row - row0], mv);
       }
-      const int rp = __shfl_up(row, 1);
-      if (in && (lane == 0 || rp != row)) atomicMax(&rmax[row - row0], mv);
     }
   }
   if (split) {

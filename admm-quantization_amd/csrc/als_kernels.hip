@@ -16,9 +16,14 @@
 // MTTKRP splits long reductions (the 9-row spatial mode has K = I J up to 262144) into
 // K chunks whose partial planes are summed in chunk order by k_als_reduce; every sum
 // is in a fixed order, so results are deterministic run to run.
+// 3-way layers with a 3 x 3 spatial mode (KD = 9) take k_als_mttkrp_sp instead: the KD
+// spatial slices are KD GEMMs that share one factor operand, W is staged in its own
+// contiguous (row, k, s) runs, and the third factor is applied in the epilogue - no
+// Khatri-Rao operand, no padded 9-row tiles, no K = I J reduction.
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/admmq.h"
@@ -30,6 +35,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kAlsBK = 16;   // K-step
 constexpr int kAlsBN = 64;   // tile columns
+constexpr int kSpatialKD = 9;   // k_als_mttkrp_sp: the flattened 3 x 3 kernel
 
 // One contraction of the batch (device descriptor).
 struct AlsJob {
@@ -49,6 +55,7 @@ struct AlsJob {
   double* epart;       // error: per-unit {sum (W-rec)^2, sum W^2}
   double* eout;        // error: caller's result slot
   int unit0, nunits;   // error: this job's unit range
+  int epi;             // MTTKRP (spatial form): 0 F = sum_s acc_s . E[s,:], 1 F[s,:] = sum_rows E . acc_s
 };
 struct AlsUnit { int job, tm, tn, ks; };
 
@@ -198,6 +205,153 @@ __global__ __launch_bounds__(Stage<BM>::NT) void k_als_mttkrp(const AlsJob* __re
   }
 }
 
+// MTTKRP of a 3-way layer W[I][J][KD] (KD = 9, the flattened 3 x 3 kernel) as KD GEMMs
+// over one shared factor operand (scripts/factorize.py:217,227,237, the einsum of W with
+// the Khatri-Rao product of the other two factors, regrouped):
+//   mode 0: acc_s[i,r] = sum_j W[i,j,s] B[j,r]     F[i,r] = sum_s acc_s[i,r] C[s,r]
+//   mode 1: acc_s[j,r] = sum_i W[i,j,s] A[i,r]     F[j,r] = sum_s acc_s[j,r] C[s,r]
+//   mode 2: acc_s[i,r] = sum_j W[i,j,s] B[j,r]     F[s,r] = sum_i A[i,r] acc_s[i,r]
+// (job: rows M, reduction K, X = the MFMA factor (K x R), Y = the epilogue factor E).
+// Per K-step the tile's W block is BM x 16 x KD floats: modes 0, 2 read each row's
+// 16 KD contiguous floats, mode 1 each reduction row's BM KD contiguous floats; it is
+// stored as KD k-major planes (the als_core image, one per s), and each B fragment read
+// from LDS feeds KD MFMAs. Mode 2 reduces over the tile's rows in the epilogue (fixed
+// order: lane rows, half-waves, waves) into one partial plane per row tile, summed in
+// tile order by k_als_reduce.
+template <int BM, int KD>
+__global__ __launch_bounds__(Stage<BM>::NT) __attribute__((amdgpu_waves_per_eu(2)))
+void k_als_mttkrp_sp(const AlsJob* __restrict__ jobs, const AlsUnit* __restrict__ units) {
+  using S = Stage<BM>;
+  static_assert(S::NT == 4 * BM && KD == 9, "36 floats (9 float4) of W per thread per K-step");
+  constexpr int PL = kAlsBK * S::LDA + 8;                 // plane stride (staggers the s planes' banks)
+  __shared__ __attribute__((aligned(16))) float sA[KD * PL];
+  __shared__ __attribute__((aligned(16))) float sB[kAlsBK * S::LDB];
+  __shared__ float red[2][KD][32];
+  const AlsUnit u = units[blockIdx.x];
+  const AlsJob& j = jobs[u.job];
+  const int m0 = u.tm * BM, n0 = u.tn * kAlsBN;
+  const int M = j.M, N = j.N, K = j.K;
+  const float* __restrict__ X = j.X;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (BM == 64) ? (wave >> 1) : 0, wn = wave & 1, i = lane & 31, h = lane >> 5;
+  // Each thread stages 36 contiguous floats of W per K-step (9 float4; the planner
+  // guarantees K % 16 == 0, M % 4 == 0, 16-byte aligned runs). Modes 0, 2 (rows are the
+  // runs): BM rows x 144 floats, thread -> row tid % BM, quarter q = tid / BM (reduction
+  // rows 4q..4q+3, all s); a wave's LDS stores then hit 64 consecutive rows. Mode 1
+  // (reduction rows are the runs): 16 runs x 9 BM floats, thread -> run tid / (BM / 4),
+  // q = tid % (BM / 4) (tile rows 4q..4q+3, all s).
+  const bool rmaj = j.afast == 0;   // block-uniform
+  int run, q;
+  if (rmaj) { run = tid % BM; q = tid / BM; }
+  else { run = tid / (BM / 4); q = tid % (BM / 4); }
+  const bool wvalid = rmaj ? (m0 + run < M) : (m0 + 4 * q < M);
+  const float* wp = rmaj ? j.W + (long long)(m0 + run) * j.sm + 36 * q
+                         : j.W + (long long)run * j.s1 + (long long)m0 * KD + 36 * q;
+  const long long kstep = rmaj ? (long long)kAlsBK * KD : (long long)kAlsBK * j.s1;   // W floats per K-step
+  // LDS image of float t (0..35) of the run: plane t % 9, at sbase + (t / 9) * (rmaj ? LDA : 1)
+  float* const sbase = sA + (rmaj ? 4 * q * S::LDA + run : run * S::LDA + 4 * q);
+  float4 ra[9];
+  float rb[S::PB];
+  auto load = [&](int ks) {
+    const float* p = wp + ks * kstep;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) ra[e] = wvalid ? gld4(p + 4 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int k0 = ks * kAlsBK;
+#pragma unroll
+    for (int e = 0; e < S::PB; ++e) {
+      const int x = tid + S::NT * e;
+      const int c = x % kAlsBN, kk = x / kAlsBN;
+      const int n = n0 + c;
+      rb[e] = n < N ? *(gcf32*)(X + (long long)(k0 + kk) * N + n) : 0.f;
+    }
+  };
+  f32x16 acc[KD];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) acc[s] = zero16();
+  const int nks = K / kAlsBK;
+  load(0);
+  for (int ks = 0; ks < nks; ++ks) {
+    __syncthreads();   // the previous K-step's fragment reads are done
+    auto stage = [&](auto step) {   // step: LDS distance of consecutive reduction / tile rows
+#pragma unroll
+      for (int e = 0; e < 9; ++e) {
+        const float f[4] = {ra[e].x, ra[e].y, ra[e].z, ra[e].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int t = 4 * e + c;
+          sbase[(t % 9) * PL + (t / 9) * decltype(step)::value] = f[c];
+        }
+      }
+    };
+    if (rmaj) stage(std::integral_constant<int, S::LDA>());
+    else stage(std::integral_constant<int, 1>());
+#pragma unroll
+    for (int e = 0; e < S::PB; ++e) {
+      const int x = tid + S::NT * e;
+      sB[(x / kAlsBN) * S::LDB + x % kAlsBN] = rb[e];
+    }
+    __syncthreads();
+    if (ks + 1 < nks) load(ks + 1);   // in flight under the MFMAs
+    const float* a = sA + 32 * wm + i;
+    const float* b = sB + 32 * wn + i;
+#pragma unroll
+    for (int q = 0; q < kAlsBK / 2; ++q) {
+      const float bv = b[(2 * q + h) * S::LDB];
+#pragma unroll
+      for (int s = 0; s < KD; ++s)
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s * PL + (2 * q + h) * S::LDA], bv, acc[s], 0, 0, 0);
+    }
+  }
+  const int col = n0 + 32 * wn + i;
+  const float* __restrict__ E = j.Y;
+  if (j.epi == 0) {   // modes 0, 1: F[row, col] = sum_s acc_s[row, col] E[s, col]
+    if (col >= N) return;
+    float ev[KD];
+#pragma unroll
+    for (int s = 0; s < KD; ++s) ev[s] = E[(long long)s * N + col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < M) {
+        float v = acc[0][r] * ev[0];
+#pragma unroll
+        for (int s = 1; s < KD; ++s) v += acc[s][r] * ev[s];
+        j.out[(long long)row * N + col] = v;
+      }
+    }
+    return;
+  }
+  // mode 2: F[s, col] (partial over this tile's rows) = sum_row E[row, col] acc_s[row, col]
+  float ev[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+    ev[r] = (row < M && col < N) ? E[(long long)row * N + col] : 0.f;
+  }
+  float v[KD];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) {
+    float t = acc[s][0] * ev[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) t += acc[s][r] * ev[r];
+    v[s] = t + __shfl_xor(t, 32);   // the two half-waves' rows (same sum on both)
+  }
+  if (BM == 64) {
+    if (wm == 1 && h == 0) {
+#pragma unroll
+      for (int s = 0; s < KD; ++s) red[wn][s][i] = v[s];
+    }
+    __syncthreads();
+    if (wm == 1) return;
+#pragma unroll
+    for (int s = 0; s < KD; ++s) v[s] += red[wn][s][i];
+  }
+  if (h != 0 || col >= N) return;
+  float* dst = j.nsplit > 1 ? j.part + (size_t)u.ks * KD * N : j.out;
+#pragma unroll
+  for (int s = 0; s < KD; ++s) dst[(size_t)s * N + col] = v[s];
+}
+
 template <int BM>
 __global__ __launch_bounds__(Stage<BM>::NT) void k_als_gram(const AlsJob* __restrict__ jobs,
                                                             const AlsUnit* __restrict__ units) {
@@ -278,7 +432,7 @@ __global__ __launch_bounds__(Stage<BM>::NT) void k_als_error(const AlsJob* __res
 // MTTKRP split-K: F = sum over chunks s (in order) of part[s]. grid.y = job.
 __global__ __launch_bounds__(256) void k_als_reduce(const AlsJob* __restrict__ jobs, const int* __restrict__ ids) {
   const AlsJob& j = jobs[ids[blockIdx.y]];
-  const size_t n = (size_t)j.M * j.N;
+  const size_t n = (size_t)(j.kind == 3 ? j.K2 : j.M) * j.N;   // spatial form: KD x R planes
   for (size_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (size_t)gridDim.x * 256) {
     float s = j.part[e];
     for (int q = 1; q < j.nsplit; ++q) s += j.part[(size_t)q * n + e];
@@ -304,7 +458,7 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 
 struct AlsPlan {
   std::vector<AlsJob> jobs;
-  std::vector<AlsUnit> units[2][3];   // [BM 32 / 64][kind]
+  std::vector<AlsUnit> units[2][4];   // [BM 32 / 64][kind] (kind 3: MTTKRP, spatial form)
   std::vector<int> split_ids;         // MTTKRP jobs with nsplit > 1
   size_t bytes = 0;
 };
@@ -344,7 +498,22 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
     std::memset(&j, 0, sizeof(j));
     j.kind = kind;
     j.W = L.W;
-    if (kind == 0) {   // MTTKRP of mode `mode` (k order: see the file header)
+    const int sp_rows = mode == 1 ? J : I, sp_red = mode == 1 ? I : J;
+    if (kind == 0 && L.ndim == 3 && Kd == kSpatialKD && sp_red % kAlsBK == 0 && sp_rows % 4 == 0 && J % 4 == 0 &&
+        (reinterpret_cast<uintptr_t>(L.W) & 15) == 0) {   // MTTKRP, spatial form (k_als_mttkrp_sp)
+      const long long JK = (long long)J * Kd;
+      j.kind = 3; j.N = R; j.K2 = Kd; j.epi = mode == 2;
+      if (mode == 1) { j.M = J; j.K = I; j.sm = Kd; j.s1 = JK; j.X = L.factors[0]; j.Y = L.factors[2]; j.afast = 1; }
+      else { j.M = I; j.K = J; j.sm = JK; j.s1 = Kd; j.X = L.factors[1]; j.Y = L.factors[mode == 0 ? 2 : 0]; j.afast = 0; }
+      if (base && !L.F) { err = "cp layer: F output missing"; return ADMMQ_ERR_ARG; }
+      j.out = L.F;
+      const int bi = bm_index(j.M), BM = bi ? 64 : 32;
+      const int tm = cdiv(j.M, BM), tn = cdiv(j.N, kAlsBN);
+      j.nsplit = mode == 2 ? tm : 1;   // mode 2: one partial plane per row tile
+      if (j.nsplit > 1) pl.split_ids.push_back(l);
+      for (int a = 0; a < tm; ++a)
+        for (int b = 0; b < tn; ++b) pl.units[bi][3].push_back({l, a, b, a});
+    } else if (kind == 0) {   // MTTKRP of mode `mode` (k order: see the file header)
       const long long JK = (long long)J * Kd;
       j.N = R;
       if (L.ndim == 3) {
@@ -391,7 +560,7 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
       j.nunits = (int)pl.units[bi][2].size() - j.unit0;
     }
     j.invK2 = 1.0f / (float)std::max(j.K2, 1);
-    if (j.K2 > 1 && (kind == 0 ? j.K : j.N) >= (1 << 24)) {   // divmod's exact range
+    if (j.kind != 3 && j.K2 > 1 && (kind == 0 ? j.K : j.N) >= (1 << 24)) {   // divmod's exact range
       err = "cp layer " + std::to_string(l) + ": Khatri-Rao index range >= 2^24";
       return ADMMQ_ERR_ARG;
     }
@@ -416,6 +585,7 @@ static int plan_als(const admmq_cp_layer* layers, int n, int mode, int kind, dou
   (void)err_units;
   for (auto& j : pl.jobs) {
     if (j.kind == 0 && j.nsplit > 1) j.part = reinterpret_cast<float*>(take((size_t)j.nsplit * j.M * j.N * 4));
+    if (j.kind == 3 && j.nsplit > 1) j.part = reinterpret_cast<float*>(take((size_t)j.nsplit * j.K2 * j.N * 4));
     if (j.kind == 2) j.epart = ep[bm_index(j.M)];
   }
   pl.bytes = off + 256;
@@ -438,16 +608,16 @@ static int run_als(const AlsPlan& pl, void* base, size_t wsb, hipStream_t s, std
   };
   std::vector<AlsUnit> all;
   all.reserve(nu);
-  size_t first[2][3];
+  size_t first[2][4];
   for (int bi = 0; bi < 2; ++bi)
-    for (int k = 0; k < 3; ++k) { first[bi][k] = all.size(); all.insert(all.end(), pl.units[bi][k].begin(), pl.units[bi][k].end()); }
+    for (int k = 0; k < 4; ++k) { first[bi][k] = all.size(); all.insert(all.end(), pl.units[bi][k].begin(), pl.units[bi][k].end()); }
   if (!up(djobs, pl.jobs.data(), pl.jobs.size() * sizeof(AlsJob)) || !up(dunits, all.data(), nu * sizeof(AlsUnit)) ||
       !up(dids, pl.split_ids.data(), pl.split_ids.size() * sizeof(int))) {
     err = "als descriptor upload failed";
     return ADMMQ_ERR_HIP;
   }
   for (int bi = 0; bi < 2; ++bi)
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
       const int n = (int)pl.units[bi][k].size();
       if (!n) continue;
       const AlsUnit* u = dunits + first[bi][k];
@@ -458,9 +628,12 @@ static int run_als(const AlsPlan& pl, void* base, size_t wsb, hipStream_t s, std
       } else if (k == 1) {
         if (bi) hipLaunchKernelGGL(k_als_gram<64>, g, t, 0, s, djobs, u);
         else hipLaunchKernelGGL(k_als_gram<32>, g, t, 0, s, djobs, u);
-      } else {
+      } else if (k == 2) {
         if (bi) hipLaunchKernelGGL(k_als_error<64>, g, t, 0, s, djobs, u);
         else hipLaunchKernelGGL(k_als_error<32>, g, t, 0, s, djobs, u);
+      } else {
+        if (bi) hipLaunchKernelGGL((k_als_mttkrp_sp<64, kSpatialKD>), g, t, 0, s, djobs, u);
+        else hipLaunchKernelGGL((k_als_mttkrp_sp<32, kSpatialKD>), g, t, 0, s, djobs, u);
       }
     }
   if (!pl.split_ids.empty()) {

@@ -1299,8 +1299,12 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
     ADMMQ_SMALL_STAMP(6);
   }
   if (stopped) return;   // (degenerate max|x|: no setup above)
-  // k_finalize_admm's step (source/admm.py:59-65) with the chosen scale
-  const QParams qp = block_qparams(kMse, bits, v, slot, ncand, 0, 0.f, 0.f);
+  // k_finalize_admm's step (source/admm.py:59-65) with the chosen scale: straight from
+  // this block's own selection (LDS) when |S| = 1, else from the canonical SSEs its
+  // stage 2 wrote (no dependent global reads of the record on the common path)
+  const QParams qp = mse_degenerate(mx) ? qparams_mse(bits, __builtin_nanf(""))
+                     : (lsel[0] == 1 ? qparams_mse(bits, cand_t(mx, lsel[2], ncand))
+                                     : block_qparams(kMse, bits, v, slot, ncand, 0, 0.f, 0.f));
   const float rho = p.rho[0];
   double s1 = 0.0, s2r = 0.0, s3 = 0.0, s4 = 0.0;
 #pragma unroll

@@ -103,6 +103,22 @@ def test_gram_mttkrp_two_way(torch_dev, shape, R):
         assert _rel(F.cpu().numpy(), Fr) < TOL, (shape, m)
 
 
+@pytest.mark.parametrize("shape,R", [((48, 40, 9), 20), ((20, 12, 9), 7), ((100, 64, 9), 300), ((96, 64, 25), 30)])
+def test_gram_mttkrp_ragged_three_way(torch_dev, shape, R):
+    """Ragged 3-way shapes: row tiles past M, R past a 64-column tile, reduction extents
+    off the 16-step (the generic Khatri-Rao path) and a 5 x 5 kernel, per mode."""
+    torch, dev = torch_dev
+    from admmq.als import gram_mttkrp
+    g = torch.Generator().manual_seed(13)
+    W = (torch.randn(*shape, generator=g) * 0.05).to(dev)
+    fs = [torch.randn(n, R, generator=g).to(dev) for n in shape]
+    for m in range(3):
+        G, F = gram_mttkrp(W, fs, m)
+        Gr, Fr = _ref64(torch, W, fs, m)
+        assert _rel(G.cpu().numpy(), Gr) < TOL, (shape, m)
+        assert _rel(F.cpu().numpy(), Fr) < TOL, (shape, m)
+
+
 def test_rel_error_reference_fixture(torch_dev):
     """The fused error reproduces the reference's recorded rec / quantized-rec errors
     for the factors it produced (F3: short ALS on layer1.0.conv1 and the 2-way case)."""

@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <array>
+#include <map>
 #include <vector>
 
 #include "../../include/admmq.h"
@@ -199,14 +201,27 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
   std::stable_sort(sorted.begin(), sorted.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
   std::vector<std::vector<GemmTile>> bins(ncu);
   std::vector<long long> load(ncu, 0);
+  // Among the least-loaded CUs, prefer the XCD (CU b mod 8) that already holds tiles of
+  // the same column tile of M (they share its B panel through that XCD's L2), then of
+  // the same row tile of P.
+  constexpr int kXcd = 8;
+  std::map<std::pair<int, int>, std::array<int, kXcd>> col_on, row_on;
   for (const GemmTile& t : sorted) {
+    auto& cx = col_on[{t.prob, t.tn}];
+    auto& rx = row_on[{t.prob, t.tm}];
     int best = -1;
+    long long best_key = 0;
     for (int b = 0; b < ncu; ++b) {
       const int cap = b < full ? rounds : rounds - 1;
-      if ((int)bins[b].size() < cap && (best < 0 || load[b] < load[best])) best = b;
+      if ((int)bins[b].size() >= cap) continue;
+      // smaller is better: load first, then affinity (column, row)
+      const long long key = load[b] * 1000000LL - cx[b % kXcd] * 1000LL - rx[b % kXcd];
+      if (best < 0 || key < best_key) { best = b; best_key = key; }
     }
     bins[best].push_back(t);
     load[best] += t.nk;
+    cx[best % kXcd] += 1;
+    rx[best % kXcd] += 1;
   }
   for (int b = 0; b < ncu; ++b)
     for (int r = 0; r < (int)bins[b].size(); ++r) tiles[b + (size_t)r * ncu] = bins[b][r];

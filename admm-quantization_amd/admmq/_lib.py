@@ -44,7 +44,8 @@ class CpLayer(ctypes.Structure):
 
 
 _lib = None
-OPS_PATH = os.path.join(_HERE, "libadmmq_torch.so")
+# ADMMQ_LIB (diagnostics, e.g. a `make TRACE=1` build): its directory also holds the ops library
+OPS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libadmmq_torch.so")
 _ops = None
 
 

@@ -189,6 +189,7 @@ size_t hist_lds_bytes(int ncand, int bits);
 size_t hist3_lds_bytes(int ncand, int bits);
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
+int copy_fin_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
 int check_thresholds(unsigned seed, int nsamp);

@@ -276,6 +276,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
+    // 32-bit element offsets inside a problem's padded buffers (admm_finalize_block)
+    if ((long long)d.Ip * d.ld >= (1LL << 31)) return fail(ADMMQ_ERR_ARG, "factor too large");
     const bool thin = a.I <= kThinRows;
     d.split = (pl.split && !thin) ? 1 : 0;
     const size_t fe = (size_t)d.Ip * d.ld;
@@ -752,6 +754,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 // diagnostics (not in include/admmq.h): per-block timelines of the last launches (make TRACE=1)
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
+int32_t admmq_debug_fin_trace(unsigned long long* host, int32_t n) { return copy_fin_trace(host, n); }
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }

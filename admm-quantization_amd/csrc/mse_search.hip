@@ -61,6 +61,13 @@ __device__ float level_threshold(float s, int k) {
 // s_memrealtime at {start, thresholds ready, elements done, flushed, end}, and the CU id.
 constexpr int kHistTraceMax = 8192;
 __device__ unsigned long long g_hist_trace[kHistTraceMax][6];
+// ... and inside its fused finalize (admm_finalize_block stamps)
+__device__ unsigned long long g_fin_trace[kHistTraceMax][4];
+int copy_fin_trace(unsigned long long* host, int n) {
+  n = n < kHistTraceMax ? n : kHistTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fin_trace), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
 
 int copy_hist_trace(unsigned long long* host, int n) {
   n = n < kHistTraceMax ? n : kHistTraceMax;
@@ -1188,7 +1195,8 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     __syncthreads();   // the search tables' LDS is reused as rmax
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) g_hist_trace[blockIdx.x][5] = ADMMQ_NOW();
     admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
-                                            blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+                                            blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem),
+                                            ADMMQ_TRACE && blockIdx.x < kHistTraceMax ? g_fin_trace[blockIdx.x] : nullptr);
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
       // columns 4, 5: {wait for the selection done, finalize done} (the search ended at 3 / 4)
       const unsigned long long tw = g_hist_trace[blockIdx.x][5];

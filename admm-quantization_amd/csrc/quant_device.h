@@ -312,6 +312,43 @@ __device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 
 }
 
 // ---------------------------------------------------------------------------
+// Wave reductions on DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then the four row
+// results read as scalars): no LDS permutes (ds_bpermute), whose waits would chain.
+// Fixed order, so the results are deterministic.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);   // out of row: 0
+}
+__device__ __forceinline__ unsigned wave_max_dpp(unsigned v) {
+  v = max(v, dpp_u32<0x111>(v));
+  v = max(v, dpp_u32<0x112>(v));
+  v = max(v, dpp_u32<0x114>(v));
+  v = max(v, dpp_u32<0x118>(v));
+  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 15), b = (unsigned)__builtin_amdgcn_readlane((int)v, 31);
+  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 47), d = (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+  return max(max(a, b), max(c, d));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {   // out of row: +0.0
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = dpp_u32<CTRL>((unsigned)b), hi = dpp_u32<CTRL>((unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0x111>(v);
+  v += dpp_f64<0x112>(v);
+  v += dpp_f64<0x114>(v);
+  v += dpp_f64<0x118>(v);
+  return (readlane_f64(v, 15) + readlane_f64(v, 31)) + (readlane_f64(v, 47) + readlane_f64(v, 63));
+}
+
+// ---------------------------------------------------------------------------
 // ADMM finalize of one unit of whole rows [start, end) of problem p (source/admm.py:58-63):
 // H = Q(X) with X = H_T - U re-formed here, U += H - H_T, the next right-hand side
 // P = F + rho (H + U) (split form: fp16 planes with the row's exponent), and the
@@ -319,39 +356,57 @@ __device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 
 // t is element start + 4 t + 4 NT g; t4 = H_T, u4 = U, h4 = H (current), f4 = F.
 // rmax: LDS of >= the unit's rows. Every thread of the block calls it. Used by
 // k_finalize_admm and by the search kernel's fused finalize (k_mse_hist3<.., true>).
+// The descriptor fields are read once into registers (the stores below would otherwise
+// force their reloads: they go through pointers that may alias the descriptor), element
+// offsets are 32-bit (a problem holds < 2^31 elements: plan_admm), stores are global.
 template <int NT, int NG>
 __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long start, long long end,
                                                     const float4* t4, const float4* u4, const float4* h4,
                                                     const float4* f4, const QParams& qp, int slot, int iter, int rep,
-                                                    unsigned* rmax) {
+                                                    unsigned* rmax, unsigned long long* trace = nullptr) {
+  // diagnostics (make TRACE=1): stamps {rho read, elements stored, row max, split stores}
+#define ADMMQ_FIN_STAMP(k) \
+  if (ADMMQ_TRACE && trace && threadIdx.x == 0) trace[k] = ADMMQ_NOW()
+  typedef __attribute__((address_space(1))) gf32x4 gst4;
   __shared__ double red[NT / 64][4];
-  const float rho = p.rho[0];
+  float* const Hd = p.H;
+  float* const Ud = p.U;
+  float* const Pd = p.P;
+  _Float16* const P2 = p.P2;
+  int* const eP = p.eP;
+  double* const res = p.res;
+  const int ld = p.ld, R = p.R;
   const bool split = p.split != 0;
-  const int row0 = (int)(start / p.ld);
+  const float rho = p.rho[0];
+  ADMMQ_FIN_STAMP(0);
+  const int s32 = (int)start, e32 = (int)end;
+  const int row0 = s32 / ld;
   if (split) {
-    const int nrows = (int)((end - start + p.ld - 1) / p.ld);
+    const int nrows = (e32 - s32 + ld - 1) / ld;
     for (int r = threadIdx.x; r < nrows; r += NT) rmax[r] = 0u;
     __syncthreads();
   }
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
   float4 p4[NG];
+  int rows[NG];
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const long long e = start + 4LL * threadIdx.x + 4LL * NT * g;
+    const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
     p4[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool in = e < end;
-    const int row = in ? (int)(e / p.ld) : 0x7FFFFFFF;
+    const bool in = e < e32;
+    const int row = e / ld;
+    rows[g] = in ? row : -1;
     if (in) {
-      const int c0 = (int)(e - (long long)row * p.ld);
+      const int c0 = e - row * ld;
       const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
       const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
       const float xs[4] = {ts[0] - us[0], ts[1] - us[1], ts[2] - us[2], ts[3] - us[3]};   // H_T - U
       const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
-      float ho[4], uo[4], po[4];
+      gf32x4 ho, uo, po;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (c0 + k < p.R) {
+        if (c0 + k < R) {
           const float hn = apply_quant(xs[k], qp);          // H = quantize(H_T - U)
           const float dh = hn - ts[k];
           const float un = us[k] + dh;                      // U += H - H_T
@@ -364,63 +419,61 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
           ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
         }
       }
-      *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
-      *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
+      *(gst4*)(Hd + e) = ho;
+      *(gst4*)(Ud + e) = uo;
       p4[g] = make_float4(po[0], po[1], po[2], po[3]);
-      if (!split) *reinterpret_cast<float4*>(p.P + e) = p4[g];
+      if (!split) *(gst4*)(Pd + e) = po;
     }
-    if (split) {   // uniform: row max of |next P| (a float4 never straddles a row, ld % 32 == 0)
-      // segmented max over the wave's lanes of one row (rows are contiguous lane ranges),
-      // then one LDS atomic per (wave, row) instead of one per lane
-      unsigned mv = __float_as_uint(fmaxf(fmaxf(fabsf(p4[g].x), fabsf(p4[g].y)), fmaxf(fabsf(p4[g].z), fabsf(p4[g].w))));
-      const int rfirst = __builtin_amdgcn_readfirstlane(row), rlast = __builtin_amdgcn_readlane(row, 63);
-      if (rfirst == rlast) {   // the whole wave in one row (rows of >= 256 elements): a plain wave max
-        mv = wave_max_u32(mv);
-        if (lane == 0 && in) atomicMax(&rmax[row - row0], mv);
-      } else {
+  }
+  if (split) {   // row max of |next P| per (wave, row): rows are contiguous lane ranges
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const unsigned o = (unsigned)__shfl_down((int)mv, off);
-          const int ro = __shfl_down(row, off);
-          if (lane + off < 64 && ro == row) mv = max(mv, o);
-        }
-        const int rp = __shfl_up(row, 1);
-        if (in && (lane == 0 || rp != row)) atomicMax(&rmax[row - row0], mv);
+    for (int g = 0; g < NG; ++g) {
+      const unsigned mv = rows[g] >= 0 ? __float_as_uint(fmaxf(fmaxf(fabsf(p4[g].x), fabsf(p4[g].y)),
+                                                               fmaxf(fabsf(p4[g].z), fabsf(p4[g].w))))
+                                       : 0u;
+      int r = __builtin_amdgcn_readfirstlane(rows[g]);   // lane 0 is in whenever any lane is
+      if (r < 0) continue;
+      for (;;) {
+        const unsigned m = wave_max_dpp(rows[g] == r ? mv : 0u);
+        if (lane == 0) atomicMax(&rmax[r - row0], m);
+        if (__ballot(rows[g] > r) == 0ull) break;
+        ++r;
       }
     }
   }
+  ADMMQ_FIN_STAMP(1);
   if (split) {
     __syncthreads();
+    ADMMQ_FIN_STAMP(2);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const long long e = start + 4LL * threadIdx.x + 4LL * NT * g;
-      if (e >= end) continue;
-      const int row = (int)(e / p.ld);
-      const int c0 = (int)(e - (long long)row * p.ld);
+      if (rows[g] < 0) continue;
+      const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
+      const int row = rows[g];
+      const int c0 = e - row * ld;
       const int ex = split_exponent(__uint_as_float(rmax[row - row0]));
-      split_store4(p.P2 + (size_t)row * 2 * p.ld, c0, p4[g], ex);
-      if (c0 == 0) p.eP[row] = ex;
+      split_store4(P2 + (size_t)row * 2 * ld, c0, p4[g], ex);
+      if (c0 == 0) eP[row] = ex;
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off);
-    s3 += __shfl_xor(s3, off); s4 += __shfl_xor(s4, off);
-  }
+  ADMMQ_FIN_STAMP(3);
+#undef ADMMQ_FIN_STAMP
+  s1 = wave_sum_dpp(s1); s2 = wave_sum_dpp(s2);
+  s3 = wave_sum_dpp(s3); s4 = wave_sum_dpp(s4);
   const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[w][0] = s1; red[w][1] = s2; red[w][2] = s3; red[w][3] = s4; }
+  if (lane == 0) { red[w][0] = s1; red[w][1] = s2; red[w][2] = s3; red[w][3] = s4; }
   __syncthreads();
   if (threadIdx.x < 4) {
     double v = 0.0;
 #pragma unroll
     for (int k = 0; k < NT / 64; ++k) v += red[k][threadIdx.x];
-    atomicAdd(&p.res[4 * (kResRep * slot + rep) + threadIdx.x], v);
+    atomicAdd(&res[4 * (kResRep * slot + rep) + threadIdx.x], v);
   }
   if (start == 0 && threadIdx.x == 0) {
     p.flags[1] = iter + 1;
     unsigned* st = p.mv.stat + 4 * (slot ^ 1);
     st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
-    double* rs = p.res + 4 * kResRep * (slot ^ 1);
+    double* rs = res + 4 * kResRep * (slot ^ 1);
     for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
   }
 }

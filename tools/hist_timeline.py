@@ -58,6 +58,28 @@ for name, j0, j1 in phases:
     print(f"  {name:13s} avg {sum(d)/len(d):7.2f}  max {max(d):7.2f} us")
 starts = sorted((r[0] - t0) / 100 for r in rows)
 print("  start offsets: median %.2f  90%% %.2f  max %.2f us" % (starts[len(starts) // 2], starts[int(0.9 * len(starts))], starts[-1]))
+if fused and hasattr(lib, "admmq_debug_fin_trace"):
+    fb = (ctypes.c_ulonglong * (4 * n))()
+    lib.admmq_debug_fin_trace(fb, n)
+    fr = [([fb[4 * b + j] for j in range(4)], rows[b]) for b in range(len(rows))]
+    fr = [(f, r) for f, r in fr if f[0] >= r[4] and f[3] >= f[0]]
+    if fr:
+        print(f"  finalize sub-phases over {len(fr)} blocks:")
+        for name, a0, a1 in (("start->rho", None, 0), ("elements+stores", 0, 1), ("rowmax barrier", 1, 2),
+                             ("split stores", 2, 3), ("residuals+end", 3, None)):
+            d = [((f[a1] if a1 is not None else r[5]) - (f[a0] if a0 is not None else r[4])) / 100 for f, r in fr]
+            print(f"    {name:16s} avg {sum(d)/len(d):6.2f}  max {max(d):6.2f} us")
+sfn = getattr(lib, "admmq_debug_setup_trace", None)
+if sfn is not None:
+    sb = (ctypes.c_ulonglong * (5 * n))()
+    sg = sfn(sb, n)
+    sr = [[sb[5 * b + k] for k in range(5)] for b in range(sg) if sb[5 * b] and sb[5 * b + 4] >= sb[5 * b]]
+    if sr:
+        print(f"  setup sub-phases over {len(sr)} blocks (kernel start -> setup start avg "
+              f"{sum((s[0] - r[0]) / 100 for s, r in zip(sr, rows)) / len(sr):.2f} us):")
+        for k, nm in enumerate(["thresholds+scatter", "ties", "check+L+cells", "(fallback)"]):
+            d = [(r[k + 1] - r[k]) / 100 for r in sr]
+            print(f"    {nm:18s} avg {sum(d) / len(d):6.2f}  max {max(d):6.2f} us")
 cus = {}
 for r in rows:
     cus.setdefault(r[5], []).append(r)

@@ -264,6 +264,11 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
     if constexpr (!PRE) load_epi();
     const int col = col0 + 32 * wn + i;
     unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+    // descriptor fields once into registers (the stores below may alias the descriptor)
+    typedef __attribute__((address_space(1))) float gf32;
+    gf32* const HTg = (gf32*)p.HT;
+    gf32* const Xg = p.X_dbg ? (gf32*)p.X : nullptr;   // X = H_T - U is re-formed by its readers; debug output only
+    const int pI = p.I, pR = p.R;
     if (col < ld) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -271,9 +276,9 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
         const size_t off = (size_t)row * ld + col;
         const float ht = SPLIT ? __builtin_ldexpf(acc[r], -(epre[r] + ecol)) : acc[r];
         const float x = ht - upre[r];
-        p.HT[off] = ht;
-        if (p.X_dbg) p.X[off] = x;   // X = H_T - U is re-formed by its readers; stored for debug output only
-        if (row < p.I && col < p.R) {
+        HTg[off] = ht;
+        if (Xg) Xg[off] = x;
+        if (row < pI && col < pR) {
           amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
           const unsigned e = enc_ord(x);
           mn = min(mn, e);

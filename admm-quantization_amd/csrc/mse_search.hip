@@ -581,9 +581,7 @@ __device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned lon
   cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
   double lo = 1e300, hi = 1e300;
   if (c < n) cx.bounds(c, t1, t2, lo, hi);
-  double m = hi;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off));
+  const double m = wave_min_f64(hi);
   if (lane == 0) wmin[w] = m;
   __syncthreads();
   double mn = wmin[0];
@@ -873,22 +871,14 @@ __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsig
       r4 += c; cntN[i] = r4;
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned long long q1 = r1, q2 = r2;
-    unsigned q3 = r3, q4 = r4;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
-      const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
-      if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
-    }
+    // wave suffix sums (DPP); the lanes above this one hold q - r
+    const unsigned long long q1 = wave_suffix_u64(r1), q2 = wave_suffix_u64(r2);
+    const unsigned q3 = wave_suffix_u32(r3), q4 = wave_suffix_u32(r4);
     if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
     __syncthreads();
-    unsigned long long a1 = 0ull, a2 = 0ull;
-    unsigned a3 = 0u, a4 = 0u;
+    unsigned long long a1 = q1 - r1, a2 = q2 - r2;
+    unsigned a3 = q3 - r3, a4 = q4 - r4;
     for (int j = w + 1; j < NW; ++j) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
-    const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
-    const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
-    if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
     for (int i = b0; i < b1; ++i) { sumA[i] += a1; sumN[i] += a2; cntA[i] += a3; cntN[i] += a4; }
     __syncthreads();
     return;
@@ -923,24 +913,16 @@ __device__ __forceinline__ void h3_suffix(int M, unsigned long long* sumA, unsig
     }
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  unsigned long long q1 = r1, q2 = r2;
-  unsigned q3 = r3, q4 = r4;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long o1 = __shfl_down(q1, off), o2 = __shfl_down(q2, off);
-    const unsigned o3 = __shfl_down(q3, off), o4 = __shfl_down(q4, off);
-    if (lane + off < 64) { q1 += o1; q2 += o2; q3 += o3; q4 += o4; }
-  }
+  // wave suffix sums (DPP); the lanes above this one hold q - r
+  const unsigned long long q1 = wave_suffix_u64(r1), q2 = wave_suffix_u64(r2);
+  const unsigned q3 = wave_suffix_u32(r3), q4 = wave_suffix_u32(r4);
   if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; wtot32[w] = q3; wtot32b[w] = q4; }
-  const unsigned long long n1 = __shfl_down(q1, 1), n2 = __shfl_down(q2, 1);
-  const unsigned n3 = __shfl_down(q3, 1), n4 = __shfl_down(q4, 1);
   __syncthreads();
-  unsigned long long a1 = 0ull, a2 = 0ull;
-  unsigned a3 = 0u, a4 = 0u;
+  unsigned long long a1 = q1 - r1, a2 = q2 - r2;
+  unsigned a3 = q3 - r3, a4 = q4 - r4;
 #pragma unroll
   for (int j = 1; j < NW; ++j)
     if (j > w) { a1 += wtot[j]; a2 += wtot2[j]; a3 += wtot32[j]; a4 += wtot32b[j]; }
-  if (lane != 63) { a1 += n1; a2 += n2; a3 += n3; a4 += n4; }
   if (inreg) {
 #pragma unroll
     for (int i = 0; i < PM; ++i) {
@@ -1084,8 +1066,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     if (t1) atomicAdd(&g1[c], t1);
     if (t2) atomicAdd(&g2[c], t2);
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+  s2 = wave_sum_f64(s2);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1293,8 +1274,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
     ADMMQ_SMALL_STAMP(4);
     unsigned long long t1 = 0ull, t2 = 0ull;   // candidate tid (n <= 1024)
     if ((int)threadIdx.x < n) h3_totals<QMAX>(threadIdx.x, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+    s2 = wave_sum_f64(s2);
     if (lane == 0) red[w] = s2;
     __syncthreads();
     double S2 = 0.0;
@@ -1313,57 +1293,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_mse_small_admm(const ProbDesc
   const QParams qp = mse_degenerate(mx) ? qparams_mse(bits, __builtin_nanf(""))
                      : (lsel[0] == 1 ? qparams_mse(bits, cand_t(mx, lsel[2], ncand))
                                      : block_qparams(kMse, bits, v, slot, ncand, 0, 0.f, 0.f));
-  const float rho = p.rho[0];
-  double s1 = 0.0, s2r = 0.0, s3 = 0.0, s4 = 0.0;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const long long e = 4LL * threadIdx.x + 4096LL * g;
-    if (e >= total) continue;
-    const int row = (int)(e / p.ld);
-    const int c0 = (int)(e - (long long)row * p.ld);
-    const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w}, hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w};
-    const float us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w}, fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
-    float ho[4], uo[4], po[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (c0 + k < p.R) {
-        const float xk = ts[k] - us[k];                   // H_T - U
-        const float hn = apply_quant(xk, qp);             // H = quantize(H_T - U)
-        const float dh = hn - ts[k];
-        const float un = us[k] + dh;                      // U += H - H_T
-        ho[k] = hn; uo[k] = un;
-        po[k] = fs[k] + rho * (hn + un);                  // next rhs F + rho(H+U)
-        const float dp = hn - hs[k];
-        s1 += (double)(dh * dh); s2r += (double)(hn * hn);
-        s3 += (double)(dp * dp); s4 += (double)(un * un);
-      } else {
-        ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
-      }
-    }
-    *reinterpret_cast<float4*>(p.H + e) = make_float4(ho[0], ho[1], ho[2], ho[3]);
-    *reinterpret_cast<float4*>(p.U + e) = make_float4(uo[0], uo[1], uo[2], uo[3]);
-    *reinterpret_cast<float4*>(p.P + e) = make_float4(po[0], po[1], po[2], po[3]);
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off); s2r += __shfl_xor(s2r, off);
-    s3 += __shfl_xor(s3, off); s4 += __shfl_xor(s4, off);
-  }
-  __shared__ double fred[16][4];
-  if (lane == 0) { fred[w][0] = s1; fred[w][1] = s2r; fred[w][2] = s3; fred[w][3] = s4; }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    double t = 0.0;
-    for (int k = 0; k < nw; ++k) t += fred[k][threadIdx.x];
-    atomicAdd(&p.res[4 * (kResRep * slot) + threadIdx.x], t);
-  }
-  if (threadIdx.x == 0) {
-    p.flags[1] = iter + 1;
-    unsigned* st = p.mv.stat + 4 * (slot ^ 1);
-    st[0] = 0u; st[1] = 0xFFFFFFFFu; st[2] = 0u; st[3] = 0u;
-    double* rs = p.res + 4 * kResRep * (slot ^ 1);
-    for (int k = 0; k < 4 * kResRep; ++k) rs[k] = 0.0;
-  }
+  admm_finalize_block<kSmallThreads, G>(p, 0, total, t4, u4, h4, f4, qp, slot, iter, 0, nullptr);   // thin: no split
   ADMMQ_SMALL_STAMP(7);
 }
 

@@ -228,15 +228,89 @@ __device__ __forceinline__ void sse_sweep_list(const float4* __restrict__ xs, in
   }
 }
 
+// Wave reductions and scans on DPP (row_shr / row_shl 1, 2, 4, 8 inside each 16-lane row,
+// then the four row results read as scalars): no LDS permutes (ds_bpermute), whose
+// waits would chain. Fixed order, so the results are deterministic.
+// dpp_zero: the neighbour's value, 0 where it lies outside the row (sums);
+// dpp_keep: ... the lane's own value there (max / min).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_zero(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_keep(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned readlane_u32(unsigned v, int l) { return (unsigned)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ unsigned long long u64_of(unsigned lo, unsigned hi) {
+  return ((unsigned long long)hi << 32) | lo;
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_zero_u64(unsigned long long v) {
+  return u64_of(dpp_zero<CTRL>((unsigned)v), dpp_zero<CTRL>((unsigned)(v >> 32)));
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  return u64_of(readlane_u32((unsigned)v, l), readlane_u32((unsigned)(v >> 32), l));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_zero_f64(double v) {   // out of row: +0.0
+  return __longlong_as_double((long long)dpp_zero_u64<CTRL>((unsigned long long)__double_as_longlong(v)));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_keep_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return __longlong_as_double((long long)u64_of(dpp_keep<CTRL>((unsigned)b), dpp_keep<CTRL>((unsigned)(b >> 32))));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double((long long)readlane_u64((unsigned long long)__double_as_longlong(v), l));
+}
+// results are wave-uniform
 __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, off));
-  return v;
+  v = max(v, dpp_keep<0x111>(v));
+  v = max(v, dpp_keep<0x112>(v));
+  v = max(v, dpp_keep<0x114>(v));
+  v = max(v, dpp_keep<0x118>(v));
+  return max(max(readlane_u32(v, 15), readlane_u32(v, 31)), max(readlane_u32(v, 47), readlane_u32(v, 63)));
 }
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off));
-  return v;
+  v = min(v, dpp_keep<0x111>(v));
+  v = min(v, dpp_keep<0x112>(v));
+  v = min(v, dpp_keep<0x114>(v));
+  v = min(v, dpp_keep<0x118>(v));
+  return min(min(readlane_u32(v, 15), readlane_u32(v, 31)), min(readlane_u32(v, 47), readlane_u32(v, 63)));
+}
+__device__ __forceinline__ double wave_min_f64(double v) {
+  v = fmin(v, dpp_keep_f64<0x111>(v));
+  v = fmin(v, dpp_keep_f64<0x112>(v));
+  v = fmin(v, dpp_keep_f64<0x114>(v));
+  v = fmin(v, dpp_keep_f64<0x118>(v));
+  return fmin(fmin(readlane_f64(v, 15), readlane_f64(v, 31)), fmin(readlane_f64(v, 47), readlane_f64(v, 63)));
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dpp_zero_f64<0x111>(v);
+  v += dpp_zero_f64<0x112>(v);
+  v += dpp_zero_f64<0x114>(v);
+  v += dpp_zero_f64<0x118>(v);
+  return (readlane_f64(v, 15) + readlane_f64(v, 31)) + (readlane_f64(v, 47) + readlane_f64(v, 63));
+}
+// inclusive suffix sums over the wave (lane l: sum over lanes >= l), row_shl steps
+__device__ __forceinline__ unsigned long long wave_suffix_u64(unsigned long long v) {
+  v += dpp_zero_u64<0x101>(v);
+  v += dpp_zero_u64<0x102>(v);
+  v += dpp_zero_u64<0x104>(v);
+  v += dpp_zero_u64<0x108>(v);
+  const unsigned long long t1 = readlane_u64(v, 16), t2 = readlane_u64(v, 32), t3 = readlane_u64(v, 48);
+  const int row = (threadIdx.x & 63) >> 4;
+  return v + (row < 1 ? t1 : 0ull) + (row < 2 ? t2 : 0ull) + (row < 3 ? t3 : 0ull);
+}
+__device__ __forceinline__ unsigned wave_suffix_u32(unsigned v) {
+  v += dpp_zero<0x101>(v);
+  v += dpp_zero<0x102>(v);
+  v += dpp_zero<0x104>(v);
+  v += dpp_zero<0x108>(v);
+  const unsigned t1 = readlane_u32(v, 16), t2 = readlane_u32(v, 32), t3 = readlane_u32(v, 48);
+  const int row = (threadIdx.x & 63) >> 4;
+  return v + (row < 1 ? t1 : 0u) + (row < 2 ? t2 : 0u) + (row < 3 ? t3 : 0u);
 }
 
 // Resolve the quantization parameters of a job inside a block (all threads call).
@@ -309,43 +383,6 @@ __device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 
   _Float16* b = dst_row + (col >> 5) * 64 + (col & 31);
   *reinterpret_cast<h4*>(b) = hi;
   *reinterpret_cast<h4*>(b + 32) = lo;
-}
-
-// ---------------------------------------------------------------------------
-// Wave reductions on DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then the four row
-// results read as scalars): no LDS permutes (ds_bpermute), whose waits would chain.
-// Fixed order, so the results are deterministic.
-template <int CTRL>
-__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
-  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);   // out of row: 0
-}
-__device__ __forceinline__ unsigned wave_max_dpp(unsigned v) {
-  v = max(v, dpp_u32<0x111>(v));
-  v = max(v, dpp_u32<0x112>(v));
-  v = max(v, dpp_u32<0x114>(v));
-  v = max(v, dpp_u32<0x118>(v));
-  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 15), b = (unsigned)__builtin_amdgcn_readlane((int)v, 31);
-  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 47), d = (unsigned)__builtin_amdgcn_readlane((int)v, 63);
-  return max(max(a, b), max(c, d));
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {   // out of row: +0.0
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const unsigned lo = dpp_u32<CTRL>((unsigned)b), hi = dpp_u32<CTRL>((unsigned)(b >> 32));
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-__device__ __forceinline__ double wave_sum_dpp(double v) {
-  v += dpp_f64<0x111>(v);
-  v += dpp_f64<0x112>(v);
-  v += dpp_f64<0x114>(v);
-  v += dpp_f64<0x118>(v);
-  return (readlane_f64(v, 15) + readlane_f64(v, 31)) + (readlane_f64(v, 47) + readlane_f64(v, 63));
 }
 
 // ---------------------------------------------------------------------------
@@ -434,7 +471,7 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
       int r = __builtin_amdgcn_readfirstlane(rows[g]);   // lane 0 is in whenever any lane is
       if (r < 0) continue;
       for (;;) {
-        const unsigned m = wave_max_dpp(rows[g] == r ? mv : 0u);
+        const unsigned m = wave_max_u32(rows[g] == r ? mv : 0u);
         if (lane == 0) atomicMax(&rmax[r - row0], m);
         if (__ballot(rows[g] > r) == 0ull) break;
         ++r;
@@ -458,8 +495,8 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
   }
   ADMMQ_FIN_STAMP(3);
 #undef ADMMQ_FIN_STAMP
-  s1 = wave_sum_dpp(s1); s2 = wave_sum_dpp(s2);
-  s3 = wave_sum_dpp(s3); s4 = wave_sum_dpp(s4);
+  s1 = wave_sum_f64(s1); s2 = wave_sum_f64(s2);
+  s3 = wave_sum_f64(s3); s4 = wave_sum_f64(s4);
   const int w = threadIdx.x >> 6;
   if (lane == 0) { red[w][0] = s1; red[w][1] = s2; red[w][2] = s3; red[w][3] = s4; }
   __syncthreads();

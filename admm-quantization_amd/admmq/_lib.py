@@ -100,6 +100,8 @@ def load() -> ctypes.CDLL:
         "admmq_cp_workspace_size": (S, [P, I32, I32]),
         "admmq_cp_gram_mttkrp": (I32, [P, I32, I32, P, S, P]),
         "admmq_cp_rel_error": (I32, [P, I32, P, P, S, P]),
+        "admmq_cp64_workspace_size": (S, [P, I32, I32]),
+        "admmq_cp64_gram_mttkrp": (I32, [P, I32, I32, P, S, P]),
         "admmq_lowrank_workspace_size": (S, [I64]),
         "admmq_lowrank_reset": (I32, [P, S, P]),
         "admmq_lowrank_pre": (I32, [P, P, P, P, P, P, I64, F32, P, S, P]),

@@ -63,10 +63,11 @@ def init_factors(tensor: torch.Tensor, rank: int, init: str = "random", device=N
             factors.append(Uu[:, :rank].to(dev))
     elif init in ("parafac", "parafac-epc"):
         from .parafac_epc import parafac, parafac_epc
+        X = tensor.to(dev)   # fp64 HIP contractions on the device (admmq.parafac_epc)
         if init == "parafac":
-            _, factors = parafac(tensor, rank=rank, init="random", random_state=seed, tol=1e-5, n_iter_max=100)
+            _, factors = parafac(X, rank=rank, init="random", random_state=seed, tol=1e-5, n_iter_max=100)
         else:
-            _, factors = parafac_epc(tensor, rank=rank, init="random", als_maxiter=50, epc_maxiter=50)
+            _, factors = parafac_epc(X, rank=rank, init="random", als_maxiter=50, epc_maxiter=50)
         factors = [f.to(device=dev, dtype=torch.float32) for f in factors]
     else:
         raise NotImplementedError(init)

@@ -10,6 +10,11 @@
 
 The ``*_batched`` forms take many layers in one launch sequence (the ALS driver
 solves mode m of every layer together). HIP only: CPU tensors raise.
+
+* ``gram_mttkrp_f64(Y, factors, mode)`` -> ``(F, G)``: the same per-mode contractions in
+  fp64 (C-ABI ``admmq_cp64_gram_mttkrp``, f64 MFMA) for the CP-ALS / EPC initialiser
+  (``admmq.parafac_epc``; tensorly ``parafac`` / musco ``cp_anc`` in the reference,
+  ``source/parafac_epc.py:42-74``).
 """
 from __future__ import annotations
 
@@ -128,3 +133,40 @@ def rel_error_batched(layers: Sequence[Tuple[torch.Tensor, Sequence[torch.Tensor
 
 def rel_error(W: torch.Tensor, factors: Sequence[torch.Tensor]) -> float:
     return rel_error_batched([(W, factors)])[0]
+
+
+def gram_mttkrp_f64(Y: torch.Tensor, factors: Sequence[torch.Tensor], mode: int
+                    ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp64 ``(F, G)`` of mode ``mode``: F = Y_(mode) . KR(other factors) (torch ``unfold``
+    / Khatri-Rao order), G = Hadamard product of the other factors' Grams. factors[mode]
+    is not read. Float64 tensors on the GPU only."""
+    if Y.dim() not in (2, 3):
+        raise ValueError(f"admmq: CP tensor must be 2-D or 3-D, got {Y.dim()}-D")
+    if len(factors) != Y.dim():
+        raise ValueError(f"admmq: {Y.dim()}-way tensor needs {Y.dim()} factors, got {len(factors)}")
+    R = factors[0].shape[1]
+    for d, f in enumerate(factors):
+        if f.dim() != 2 or f.shape != (Y.shape[d], R):
+            raise ValueError(f"admmq: factor {d} has shape {tuple(f.shape)}, expected {(Y.shape[d], R)}")
+    for t in (Y, *factors):
+        if t.device.type != "cuda" or t.dtype != torch.float64:
+            raise RuntimeError("admmq: the fp64 CP contractions need float64 tensors on a ROCm GPU (no CPU path)")
+    Y = Y.contiguous()
+    fs = [f.contiguous() for f in factors]
+    F = torch.empty(Y.shape[mode], R, dtype=torch.float64, device=Y.device)
+    G = torch.empty(R, R, dtype=torch.float64, device=Y.device)
+    L = _lib.CpLayer()   # admmq_cp_layer_f64 has admmq_cp_layer's layout
+    L.W = Y.data_ptr()
+    for d in range(3):
+        L.factors[d] = fs[d].data_ptr() if d < len(fs) else None
+        L.dims[d] = Y.shape[d] if d < Y.dim() else 0
+    L.G, L.F, L.ndim, L.R = G.data_ptr(), F.data_ptr(), Y.dim(), R
+    lib = _lib.load()
+    arr = (_lib.CpLayer * 1)(L)
+    nbytes = lib.admmq_cp64_workspace_size(arr, 1, mode)
+    if nbytes == 0:
+        _lib.check(1, "cp64_workspace_size")
+    ws = _lib.workspace(nbytes, Y.device)
+    _lib.check(lib.admmq_cp64_gram_mttkrp(arr, 1, mode, _lib.ptr(ws), ws.numel(), _lib.stream_handle(Y.device)),
+               "cp64_gram_mttkrp")
+    return F, G

@@ -1,0 +1,327 @@
+// fp64 per-mode contractions of the CP-ALS / EPC initialiser (admmq.parafac_epc; the
+// reference's source/parafac_epc.py:42-74 runs them inside tensorly `parafac` and musco
+// `cp_anc` on the fp64 tensor):
+//
+//   MTTKRP  F[a, r] = sum_k Y_(n)[a, k] KR[k, r]      KR = Khatri-Rao product of the other factors
+//   Gram    G = hadamard over o != n of (U_o^T U_o)
+//
+// on v_mfma_f64_16x16x4_f64: a 64 x 64 output tile per workgroup of 4 waves (each wave a
+// 32 x 32 sub-tile = 2 x 2 MFMA blocks), K-step 16 staged through registers into
+// double-buffered k-major LDS images (one barrier per step). As in the fp32 ALS kernels
+// (als_kernels.hip), the Khatri-Rao operand is formed while the K-step is staged and the
+// unfolding is addressed in place - nothing is materialised; long reductions are split
+// into K chunks whose partial planes k_cp64_reduce sums in chunk order (deterministic).
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/admmq.h"
+#include "admmq_internal.h"
+
+namespace admmq {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kC64BM = 64, kC64BN = 64, kC64BK = 16, kC64NT = 256;
+constexpr int kC64LD = kC64BM + 8;   // LDS row stride (doubles): the 4 k rows of a fragment read on distinct banks
+constexpr int kC64PA = kC64BK * kC64BM / kC64NT;   // A elements per thread per K-step
+constexpr int kC64PB = kC64BK * kC64BN / kC64NT;   // B elements per thread per K-step
+
+struct Cp64Job {
+  int kind;             // 0 MTTKRP, 1 Gram(-Hadamard)
+  int M, N, K;          // output rows / cols, reduction length (MTTKRP)
+  int nsplit, kchunk;   // MTTKRP: K chunks and their length (multiple of kC64BK)
+  int K2;               // MTTKRP: Khatri-Rao inner extent (1: one other factor, 2-way)
+  int afast;            // A side staged along rows (rows contiguous in memory)
+  int R, Kx, Ky;        // Gram: rank, rows of X, rows of Y (0: no Hadamard factor)
+  int pad_;
+  long long sm, s1, s2; // MTTKRP: Y_(n)[a, k] = W[a sm + (k / K2) s1 + (k % K2) s2]
+  const double* W;
+  const double* X;      // MTTKRP: KR outer factor ((K / K2) x N); Gram: first factor (Kx x R)
+  const double* Y;      // MTTKRP: KR inner factor (K2 x N) or nullptr; Gram: second factor or nullptr
+  double* part;         // MTTKRP: [nsplit][M][N] partial planes (nsplit > 1)
+  double* out;          // MTTKRP: F (M x N); Gram: G (R x R)
+};
+struct Cp64Unit { int job, tm, tn, ks; };
+
+__device__ __forceinline__ double c64_opA(const Cp64Job& j, int which, int m, int k) {
+  if (j.kind == 0) {
+    const int kq = k / j.K2, kr = k - kq * j.K2;
+    return j.W[(long long)m * j.sm + (long long)kq * j.s1 + (long long)kr * j.s2];
+  }
+  return (which ? j.Y : j.X)[(long long)k * j.R + m];   // A(m = r1, k = i) = U[i, r1]
+}
+__device__ __forceinline__ double c64_opB(const Cp64Job& j, int which, int k, int n) {
+  if (j.kind == 0) {
+    if (j.K2 == 1) return j.X[(long long)k * j.N + n];
+    const int kq = k / j.K2, kr = k - kq * j.K2;
+    return j.X[(long long)kq * j.N + n] * j.Y[(long long)kr * j.N + n];
+  }
+  return (which ? j.Y : j.X)[(long long)k * j.R + n];
+}
+
+// acc[i][c] (the 16 x 16 MFMA block (i, c) of this wave's 32 x 32 sub-tile of the tile at
+// (m0, n0)) += sum over k in [kb, ke) of A(m, k) B(k, n).
+__device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, int n0, int kb, int ke, int Mrows,
+                                         int Ncols, f64x4 (&acc)[2][2], double (*sA)[kC64BK * kC64LD],
+                                         double (*sB)[kC64BK * kC64LD]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool afast = j.afast != 0;
+  double ra[kC64PA], rb[kC64PB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < kC64PA; ++e) {
+      const int x = tid + kC64NT * e;
+      const int r = afast ? x % kC64BM : x / kC64BK, kk = afast ? x / kC64BM : x % kC64BK;
+      const int m = m0 + r, k = k0 + kk;
+      ra[e] = (m < Mrows && k < ke) ? c64_opA(j, which, m, k) : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < kC64PB; ++e) {
+      const int x = tid + kC64NT * e;
+      const int c = x % kC64BN, kk = x / kC64BN;
+      const int n = n0 + c, k = k0 + kk;
+      rb[e] = (n < Ncols && k < ke) ? c64_opB(j, which, k, n) : 0.0;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < kC64PA; ++e) {
+      const int x = tid + kC64NT * e;
+      const int r = afast ? x % kC64BM : x / kC64BK, kk = afast ? x / kC64BM : x % kC64BK;
+      sA[buf][kk * kC64LD + r] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < kC64PB; ++e) {
+      const int x = tid + kC64NT * e;
+      sB[buf][(x / kC64BN) * kC64LD + x % kC64BN] = rb[e];
+    }
+  };
+  if (kb >= ke) return;
+  load(kb);
+  __syncthreads();   // the previous use of the images (an earlier core call) is done
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  const int fr = lane & 15, fk = lane >> 4;   // f64 16x16x4 operands: A[fr][fk], B[fk][fr]
+  for (int k0 = kb; k0 < ke; k0 += kC64BK) {
+    const bool more = k0 + kC64BK < ke;
+    if (more) load(k0 + kC64BK);
+    const double* a = sA[buf] + 32 * wm + fr;
+    const double* b = sB[buf] + 32 * wn + fr;
+#pragma unroll
+    for (int q = 0; q < kC64BK / 4; ++q) {
+      const int kk = (4 * q + fk) * kC64LD;
+      const double a0 = a[kk], a1 = a[kk + 16], b0 = b[kk], b1 = b[kk + 16];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+}
+
+__device__ __forceinline__ void c64_zero(f64x4 (&acc)[2][2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[i][c] = f64x4{0.0, 0.0, 0.0, 0.0};
+}
+
+// One 64 x 64 output tile (and K chunk) per workgroup. C/D map of v_mfma_f64_16x16x4_f64:
+// col = lane & 15, row = (lane >> 4) + 4 reg (cdna_hip_programming.md, fragment layout).
+__global__ __launch_bounds__(kC64NT) void k_cp64(const Cp64Job* __restrict__ jobs, const Cp64Unit* __restrict__ units) {
+  __shared__ __attribute__((aligned(16))) double sA[2][kC64BK * kC64LD];
+  __shared__ __attribute__((aligned(16))) double sB[2][kC64BK * kC64LD];
+  const Cp64Unit u = units[blockIdx.x];
+  const Cp64Job& j = jobs[u.job];
+  const int m0 = u.tm * kC64BM, n0 = u.tn * kC64BN;
+  f64x4 acc[2][2];
+  c64_zero(acc);
+  double* dst;
+  if (j.kind == 0) {
+    const int kb = u.ks * j.kchunk, ke = min(j.K, kb + j.kchunk);
+    c64_core(j, 0, m0, n0, kb, ke, j.M, j.N, acc, sA, sB);
+    dst = j.nsplit > 1 ? j.part + (size_t)u.ks * j.M * j.N : j.out;
+  } else {
+    c64_core(j, 0, m0, n0, 0, j.Kx, j.R, j.R, acc, sA, sB);
+    if (j.Ky > 0) {   // Hadamard product with the second Gram (same tile)
+      f64x4 acc2[2][2];
+      c64_zero(acc2);
+      c64_core(j, 1, m0, n0, 0, j.Ky, j.R, j.R, acc2, sA, sB);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[i][c] *= acc2[i][c];
+    }
+    dst = j.out;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = n0 + 32 * wn + 16 * c + (lane & 15);
+      if (col >= j.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 32 * wm + 16 * i + (lane >> 4) + 4 * r;
+        if (row < j.M) dst[(size_t)row * j.N + col] = acc[i][c][r];
+      }
+    }
+}
+
+// MTTKRP split-K: F = sum over chunks s (in order) of part[s]. grid.y = job.
+__global__ __launch_bounds__(256) void k_cp64_reduce(const Cp64Job* __restrict__ jobs, const int* __restrict__ ids) {
+  const Cp64Job& j = jobs[ids[blockIdx.y]];
+  const size_t n = (size_t)j.M * j.N;
+  for (size_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (size_t)gridDim.x * 256) {
+    double s = j.part[e];
+    for (int q = 1; q < j.nsplit; ++q) s += j.part[(size_t)q * n + e];
+    j.out[e] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Host planning
+
+static inline size_t al64(size_t v) { return (v + 255) / 256 * 256; }
+static inline int cdiv64(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+struct Cp64Plan {
+  std::vector<Cp64Job> jobs;
+  std::vector<Cp64Unit> units;
+  std::vector<int> split_ids;
+  size_t bytes = 0;
+};
+
+static bool layer64_ok(const admmq_cp_layer_f64& L) {
+  if (!L.W || (L.ndim != 2 && L.ndim != 3) || L.R < 1) return false;
+  for (int d = 0; d < L.ndim; ++d)
+    if (L.dims[d] < 1 || !L.factors[d]) return false;
+  return true;
+}
+
+// Carve order: [jobs][units][split ids][partials]. Per layer: the mode's Gram(-Hadamard)
+// job, then its MTTKRP job (K chunks: enough units to fill the chip, chunks >= 512 rows).
+static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* base, Cp64Plan& pl, std::string& err) {
+  pl.jobs.clear(); pl.units.clear(); pl.split_ids.clear();
+  for (int l = 0; l < n; ++l) {
+    const admmq_cp_layer_f64& L = layers[l];
+    if (!layer64_ok(L)) { err = "cp64 layer " + std::to_string(l) + ": bad W/factors/dims/ndim/R"; return ADMMQ_ERR_ARG; }
+    if (mode < 0 || mode >= L.ndim) { err = "mode out of range"; return ADMMQ_ERR_ARG; }
+    const int I = L.dims[0], J = L.dims[1], Kd = L.ndim == 3 ? L.dims[2] : 1, R = L.R;
+    if ((long long)I * J * Kd >= (1LL << 31)) { err = "cp64 layer too large"; return ADMMQ_ERR_ARG; }
+    if (base && (!L.F || !L.G)) { err = "cp64 layer: F / G output missing"; return ADMMQ_ERR_ARG; }
+    Cp64Job g;
+    std::memset(&g, 0, sizeof(g));
+    g.kind = 1; g.R = R; g.M = g.N = R; g.afast = 1;
+    int o[2], no = 0;
+    for (int d = 0; d < L.ndim; ++d)
+      if (d != mode) o[no++] = d;
+    g.X = L.factors[o[0]]; g.Kx = L.dims[o[0]];
+    if (no == 2) { g.Y = L.factors[o[1]]; g.Ky = L.dims[o[1]]; }
+    g.out = L.G;
+    const int gid = (int)pl.jobs.size();
+    pl.jobs.push_back(g);
+    for (int a = 0; a < cdiv64(R, kC64BM); ++a)
+      for (int b = 0; b < cdiv64(R, kC64BN); ++b) pl.units.push_back({gid, a, b, 0});
+    Cp64Job f;
+    std::memset(&f, 0, sizeof(f));
+    f.kind = 0; f.N = R; f.W = L.W; f.M = L.dims[mode];
+    const long long JK = (long long)J * Kd;
+    if (L.ndim == 3) {   // k runs over the other two modes in their order (torch unfold / Khatri-Rao order)
+      if (mode == 0) { f.K = J * Kd; f.K2 = Kd; f.sm = JK; f.s1 = Kd; f.s2 = 1; f.X = L.factors[1]; f.Y = L.factors[2]; }
+      if (mode == 1) { f.K = I * Kd; f.K2 = Kd; f.sm = Kd; f.s1 = JK; f.s2 = 1; f.X = L.factors[0]; f.Y = L.factors[2]; }
+      if (mode == 2) { f.K = I * J; f.K2 = J; f.sm = 1; f.s1 = JK; f.s2 = Kd; f.X = L.factors[0]; f.Y = L.factors[1]; f.afast = 1; }
+    } else {
+      f.K2 = 1;
+      if (mode == 0) { f.K = J; f.sm = J; f.s1 = 1; f.X = L.factors[1]; }
+      else { f.K = I; f.sm = 1; f.s1 = J; f.X = L.factors[0]; f.afast = 1; }
+    }
+    f.out = L.F;
+    const int tm = cdiv64(f.M, kC64BM), tn = cdiv64(f.N, kC64BN);
+    const int by_k = std::max(1, f.K / 512), by_fill = std::max(1, 512 / std::max(tm * tn, 1));
+    f.nsplit = std::max(1, std::min(by_k, by_fill));
+    f.kchunk = cdiv64(cdiv64(f.K, f.nsplit), kC64BK) * kC64BK;
+    f.nsplit = cdiv64(f.K, f.kchunk);
+    const int fid = (int)pl.jobs.size();
+    if (f.nsplit > 1) pl.split_ids.push_back(fid);
+    pl.jobs.push_back(f);
+    for (int ks = 0; ks < f.nsplit; ++ks)
+      for (int a = 0; a < tm; ++a)
+        for (int b = 0; b < tn; ++b) pl.units.push_back({fid, a, b, ks});
+  }
+  size_t off = 0;
+  char* b = static_cast<char*>(base);
+  auto take = [&](size_t nbytes) -> char* { char* p = b ? b + off : nullptr; off += al64(nbytes); return p; };
+  take(pl.jobs.size() * sizeof(Cp64Job));
+  take(pl.units.size() * sizeof(Cp64Unit));
+  take(pl.split_ids.size() * sizeof(int) + 4);
+  for (auto& j : pl.jobs)
+    if (j.kind == 0 && j.nsplit > 1) j.part = reinterpret_cast<double*>(take((size_t)j.nsplit * j.M * j.N * 8));
+  pl.bytes = off + 256;
+  return ADMMQ_OK;
+}
+
+static int run_cp64(const Cp64Plan& pl, void* base, size_t wsb, hipStream_t s, std::string& err) {
+  if (!base || wsb < pl.bytes) { err = "workspace too small"; return ADMMQ_ERR_WORKSPACE; }
+  size_t off = 0;
+  char* b = static_cast<char*>(base);
+  auto take = [&](size_t nbytes) -> char* { char* p = b + off; off += al64(nbytes); return p; };
+  Cp64Job* djobs = reinterpret_cast<Cp64Job*>(take(pl.jobs.size() * sizeof(Cp64Job)));
+  Cp64Unit* dunits = reinterpret_cast<Cp64Unit*>(take(pl.units.size() * sizeof(Cp64Unit)));
+  int* dids = reinterpret_cast<int*>(take(pl.split_ids.size() * sizeof(int) + 4));
+  auto up = [&](void* dst, const void* src, size_t nbytes) {
+    return nbytes == 0 || hipMemcpyAsync(dst, src, nbytes, hipMemcpyHostToDevice, s) == hipSuccess;
+  };
+  if (!up(djobs, pl.jobs.data(), pl.jobs.size() * sizeof(Cp64Job)) ||
+      !up(dunits, pl.units.data(), pl.units.size() * sizeof(Cp64Unit)) ||
+      !up(dids, pl.split_ids.data(), pl.split_ids.size() * sizeof(int))) {
+    err = "cp64 descriptor upload failed";
+    return ADMMQ_ERR_HIP;
+  }
+  if (!pl.units.empty())
+    hipLaunchKernelGGL(k_cp64, dim3((unsigned)pl.units.size()), dim3(kC64NT), 0, s, djobs, dunits);
+  if (!pl.split_ids.empty()) {
+    size_t mx = 0;
+    for (int id : pl.split_ids) mx = std::max(mx, (size_t)pl.jobs[id].M * pl.jobs[id].N);
+    const int nb = (int)std::min<size_t>(256, (mx + 255) / 256);
+    hipLaunchKernelGGL(k_cp64_reduce, dim3(nb, (unsigned)pl.split_ids.size()), dim3(256), 0, s, djobs, dids);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { err = std::string("cp64 launch: ") + hipGetErrorString(e); return ADMMQ_ERR_HIP; }
+  return ADMMQ_OK;
+}
+
+}  // namespace admmq
+
+using namespace admmq;
+
+extern "C" {
+
+size_t admmq_cp64_workspace_size(const admmq_cp_layer_f64* layers, int32_t n, int32_t mode) {
+  Cp64Plan pl;
+  std::string err;
+  if (n < 0 || (n > 0 && !layers) || plan_cp64(layers, n, mode, nullptr, pl, err)) return 0;
+  return pl.bytes;
+}
+
+int32_t admmq_cp64_gram_mttkrp(const admmq_cp_layer_f64* layers, int32_t n, int32_t mode, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  if (n < 0 || (n > 0 && !layers)) return set_error(ADMMQ_ERR_ARG, "cp64_gram_mttkrp: bad layer array");
+  Cp64Plan pl;
+  std::string err;
+  int rc = plan_cp64(layers, n, mode, workspace, pl, err);
+  if (!rc) rc = run_cp64(pl, workspace, workspace_bytes, static_cast<hipStream_t>(stream), err);
+  if (rc) return set_error(rc, ("cp64_gram_mttkrp: " + err).c_str());
+  return ADMMQ_OK;
+}
+
+}  // extern "C"

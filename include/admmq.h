@@ -161,6 +161,27 @@ int32_t admmq_cp_gram_mttkrp(const admmq_cp_layer* layers, int32_t n, int32_t mo
 int32_t admmq_cp_rel_error(const admmq_cp_layer* layers, int32_t n, double* out, void* workspace,
                            size_t workspace_bytes, void* stream);
 
+/* fp64 per-mode contractions of the CP-ALS / EPC initialiser (admmq.parafac_epc): the
+ * reference runs them inside tensorly `parafac` and musco `cp_anc` on the fp64 tensor
+ * (source/parafac_epc.py:36-74). Same layout as admmq_cp_layer, in double. */
+typedef struct admmq_cp_layer_f64 {
+  const double* W;
+  const double* factors[3]; /* factors[2] unused (NULL) when ndim == 2 */
+  double* G;                /* R x R: Hadamard product of the Grams of the factors other than `mode` */
+  double* F;                /* dims[mode] x R: MTTKRP of W with the Khatri-Rao product of the others */
+  int32_t dims[3];
+  int32_t ndim;             /* 2 or 3 */
+  int32_t R;
+} admmq_cp_layer_f64;
+
+/* Workspace bytes for admmq_cp64_gram_mttkrp (this mode) on these layers. */
+size_t admmq_cp64_workspace_size(const admmq_cp_layer_f64* layers, int32_t n, int32_t mode);
+
+/* For every layer: G and F of `mode` in fp64 (f64 MFMA, Khatri-Rao operand formed on the
+ * fly, deterministic split-K). factors[mode] is not read. */
+int32_t admmq_cp64_gram_mttkrp(const admmq_cp_layer_f64* layers, int32_t n, int32_t mode, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* Quant + low-rank ADMM (scripts/factorize_lowrank.py:85-101), one iteration =
  *   admmq_lowrank_pre   Hbar = (rho (H + U) + W - H2) / (1 + rho),  X = Hbar - U
  *   (caller)            Hn = proj(X)   (quantizer: admmq_quantize_batched; or a rank projection)

@@ -1,0 +1,99 @@
+"""fp64 HIP contractions of the CP-ALS / EPC initialiser (csrc/cp64_kernels.hip via
+admmq.als.gram_mttkrp_f64) and admmq.parafac_epc on them, against the CPU oracle
+(oracle/epc_oracle.py, fp64 torch). source/parafac_epc.py:12-82.
+
+Parity unpinned against the reference itself (tensorly / musco absent offline): the
+contractions are checked against fp64 einsum (1e-12 relative: fp64 with another
+summation order), the drivers against the oracle's run of the same algorithm from the
+same random start (agreement to fp64 rounding drift, 1e-6 on the factors)."""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+from oracle import epc_oracle as eo
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-300))
+
+
+@pytest.mark.parametrize("shape,R", [((7, 6, 5), 3), ((64, 64, 9), 134), ((9, 64, 64), 134), ((128, 64, 9), 183),
+                                     ((512, 512, 9), 1141), ((64, 48), 13), ((300, 2048), 200), ((1, 17, 3), 40)])
+def test_cp64_gram_mttkrp_vs_einsum(shape, R):
+    from admmq.als import gram_mttkrp_f64
+    g = torch.Generator().manual_seed(sum(shape) + R)
+    Y = torch.randn(*shape, generator=g, dtype=torch.float64)
+    fs = [torch.randn(n, R, generator=g, dtype=torch.float64) for n in shape]
+    dev = torch.device("cuda:0")
+    for mode in range(len(shape)):
+        F, G = gram_mttkrp_f64(Y.to(dev), [f.to(dev) for f in fs], mode)
+        Fo, Go = eo._mttkrp_gram(Y, fs, mode)
+        assert _rel(F, Fo) < 1e-12, (shape, mode, _rel(F, Fo))
+        assert _rel(G, Go) < 1e-12, (shape, mode, _rel(G, Go))
+
+
+def _lowrank(shape, R, noise, seed):
+    g = torch.Generator().manual_seed(seed)
+    fs = [torch.randn(n, R, generator=g, dtype=torch.float64) for n in shape]
+    Y = eo._reconstruct(None, fs)
+    return Y + noise * torch.randn(*shape, generator=g, dtype=torch.float64) * Y.norm() / Y.numel() ** 0.5
+
+
+def test_parafac_matches_oracle():
+    from admmq import parafac_epc as pe
+    Y = _lowrank((10, 8, 9), 4, 0.1, 7)
+    w, fs = pe.parafac(Y.cuda(), 4, random_state=2, tol=1e-12, n_iter_max=30, normalize_factors=True)
+    wo, fso = eo.parafac(Y, 4, random_state=2, tol=1e-12, n_iter_max=30, normalize_factors=True)
+    assert _rel(w, wo) < 1e-6
+    for f, fo in zip(fs, fso):
+        assert _rel(f, fo) < 1e-6
+    rel = float((Y - eo._reconstruct(w.cpu(), [f.cpu() for f in fs])).norm() / Y.norm())
+    assert rel < 0.2
+
+
+def test_cp_anc_and_parafac_epc_match_oracle():
+    from admmq import parafac_epc as pe
+    Y = _lowrank((9, 8, 6), 6, 0.3, 2)       # over-parameterised: ALS intensities can blow up
+    w, fs = eo.parafac(Y, 6, random_state=3, tol=1e-10, n_iter_max=200, normalize_factors=True)
+    delta = float((Y - eo._reconstruct(w, fs)).norm())
+    w2, fs2 = pe.cp_anc(Y.cuda(), 6, delta, w.cuda(), [f.cuda() for f in fs], maxiter=100, tol=1e-9)
+    w2o, fs2o = eo.cp_anc(Y, 6, delta, w, fs, maxiter=100, tol=1e-9)
+    err = float((Y - eo._reconstruct(w2.cpu(), [f.cpu() for f in fs2])).norm())
+    assert err <= delta * (1 + 1e-6)
+    assert float(w2.norm()) <= float(w.norm()) * (1 + 1e-9)
+    assert _rel(w2, w2o) < 1e-6
+    Y3 = _lowrank((10, 4, 9), 5, 0.2, 4)     # modes unsorted: the driver permutes and restores
+    lam, Us = pe.parafac_epc(Y3.cuda(), 5, als_maxiter=100, epc_maxiter=30, epc_rounds=3)
+    lamo, Uso = eo.parafac_epc(Y3, 5, als_maxiter=100, epc_maxiter=30, epc_rounds=3)
+    assert [tuple(u.shape) for u in Us] == [(10, 5), (4, 5), (9, 5)]
+    assert _rel(lam, lamo) < 1e-6
+    for u, uo in zip(Us, Uso):
+        assert _rel(u, uo) < 1e-6
+
+
+def test_parafac_epc_resnet18_layer_timing():
+    """init_factors('parafac-epc')'s call (50 ALS + 50 EPC iterations per round,
+    source/admm.py:40-44) on layer1.0.conv1 (64, 64, 9), R = 134: runs on the device,
+    keeps the ALS error (EPC), reports its wall time."""
+    from admmq import synthetic
+    from admmq.parafac_epc import parafac, parafac_epc
+    idx, spec = synthetic.find_layer("resnet18", "layer1.0.conv1")
+    W = torch.from_numpy(synthetic.layer_weight(spec, idx)).cuda().double()
+    R = spec.rank()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    lam, Us = parafac_epc(W, R, als_maxiter=50, epc_maxiter=50)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    w, fs = parafac(W, R, tol=1e-5, n_iter_max=50, normalize_factors=True)
+    als_err = float((W - eo._reconstruct(w, fs)).norm() / W.norm())
+    epc_err = float((W - eo._reconstruct(lam, Us)).norm() / W.norm())
+    print(f"parafac-epc layer1.0.conv1 R={R}: {t:.2f} s, ALS rel err {als_err:.4f}, EPC rel err {epc_err:.4f}")
+    assert np.isfinite(epc_err) and epc_err <= als_err * (1 + 1e-6)

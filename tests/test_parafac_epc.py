@@ -1,13 +1,15 @@
-"""CP-ALS and CP-EPC initialisers (admmq.parafac_epc, source/parafac_epc.py:12-82).
+"""The CPU oracle of the CP-ALS and CP-EPC initialisers (oracle/epc_oracle.py; the
+product admmq.parafac_epc runs the same algorithm on the fp64 HIP contractions and is
+checked against this oracle in tests/test_gpu_epc.py). source/parafac_epc.py:12-82.
 
 Parity unpinned (tensorly / musco-pytorch absent offline): these are
 objective-level checks of the published algorithms - the EPC result keeps the ALS
 reconstruction error (||Y - [[lambda; U]]|| <= delta) while not increasing the
-intensities ||lambda||, with unit-norm factor columns and the reference's return layout.
-fp64 torch on CPU (an initialiser; no HIP kernel involved)."""
+intensities ||lambda||, with unit-norm factor columns and the reference's return layout."""
+import pytest
 import torch
 
-from admmq.parafac_epc import _reconstruct, cp_anc, parafac, parafac_epc
+from oracle.epc_oracle import _reconstruct, cp_anc, parafac, parafac_epc
 
 
 def _lowrank(shape, R, noise, seed):
@@ -49,3 +51,10 @@ def test_parafac_epc_layout_and_objective():
     epc_err = float((Y - _reconstruct(lam, Us)).norm())
     assert epc_err <= als_err * (1 + 1e-6)
     assert float(lam.norm()) <= float(w.norm()) * (1 + 1e-9)
+
+
+def test_product_has_no_cpu_path():
+    """admmq.parafac_epc is the HIP product: a CPU tensor raises instead of running on the host."""
+    from admmq import parafac_epc as product
+    with pytest.raises(RuntimeError):
+        product.parafac(torch.zeros(3, 4, 5, dtype=torch.float64), 2, n_iter_max=1)

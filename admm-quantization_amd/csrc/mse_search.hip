@@ -62,10 +62,10 @@ __device__ float level_threshold(float s, int k) {
 constexpr int kHistTraceMax = 8192;
 __device__ unsigned long long g_hist_trace[kHistTraceMax][6];
 // ... and inside its fused finalize (admm_finalize_block stamps)
-__device__ unsigned long long g_fin_trace[kHistTraceMax][4];
+__device__ unsigned long long g_fin_trace[kHistTraceMax][5];
 int copy_fin_trace(unsigned long long* host, int n) {
   n = n < kHistTraceMax ? n : kHistTraceMax;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fin_trace), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fin_trace), (size_t)n * 5 * sizeof(unsigned long long)) == hipSuccess
              ? n : -1;
 }
 

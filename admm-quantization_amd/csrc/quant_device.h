@@ -50,6 +50,8 @@ struct QParams {
   int zp;
   float mn, rng, n;
   int nan_all;
+  float rcp;    // MSE: 1 / scale (IEEE), for apply_quant_mse's reciprocal fast path
+  int fast;     // MSE: the fast path is valid (scale and 1 / scale normal and finite)
 };
 
 __device__ __forceinline__ float nan_clamp(float q, float lo, float hi) {
@@ -110,6 +112,9 @@ __device__ __forceinline__ QParams qparams_mse(int bits, float t) {
   p.scale = (2.0f * t) / (float)(2 * q - 1);
   p.nan_all = (t == t) ? 0 : 1;
   p.zp = 0; p.mn = 0.f; p.rng = 0.f; p.n = 0.f;
+  p.rcp = 1.0f / p.scale;
+  const float as = __builtin_fabsf(p.scale), ar = __builtin_fabsf(p.rcp);
+  p.fast = (as >= 0x1p-126f && as < __builtin_inff() && ar >= 0x1p-126f && ar < __builtin_inff()) ? 1 : 0;
   return p;
 }
 
@@ -137,6 +142,21 @@ __device__ __forceinline__ float apply_quant(float x, const QParams& p) {
   const float r = (x - p.mn) / p.rng;
   const float qi = __builtin_floorf(r * p.n + 0.5f);
   return (qi * p.rng) / p.n + p.mn;
+}
+
+// The MSE projection clamp(rint(fl(x / s)), qlo, qhi) * s with the quotient from the
+// reciprocal: y = x * (1 / s) is within |y| 2^-23 of x / s (two roundings), so rint(y)
+// is rint(fl(x / s)) unless y lies within |y| 2^-21 of a half-integer - then the IEEE
+// quotient decides (rare). NaN / inf inputs take the same values either way; a
+// non-normal scale or reciprocal (p.fast == 0) always divides. Same bits as
+// apply_quant (GPU parity tests).
+__device__ __forceinline__ float apply_quant_mse(float x, const QParams& p) {
+  if (p.nan_all) return __builtin_nanf("");
+  const float y = x * p.rcp;
+  float q = __builtin_rintf(y);
+  if (!p.fast || __builtin_fabsf(__builtin_fabsf(y - q) - 0.5f) < __builtin_fabsf(y) * 0x1p-21f)
+    q = __builtin_rintf(x / p.scale);
+  return nan_clamp(q, p.qlo, p.qhi) * p.scale;
 }
 
 // First-index argmin of sse[0..n) by ONE wave (all 64 lanes must call).
@@ -401,7 +421,8 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
                                                     const float4* t4, const float4* u4, const float4* h4,
                                                     const float4* f4, const QParams& qp, int slot, int iter, int rep,
                                                     unsigned* rmax, unsigned long long* trace = nullptr) {
-  // diagnostics (make TRACE=1): stamps {rho read, elements stored, row max, split stores}
+  // diagnostics (make TRACE=1): stamps {rho read, elements stored, row max, split stores,
+  // the block's loads complete (before the elements; trace builds wait for them there)}
 #define ADMMQ_FIN_STAMP(k) \
   if (ADMMQ_TRACE && trace && threadIdx.x == 0) trace[k] = ADMMQ_NOW()
   typedef __attribute__((address_space(1))) gf32x4 gst4;
@@ -414,6 +435,7 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
   double* const res = p.res;
   const int ld = p.ld, R = p.R;
   const bool split = p.split != 0;
+  const bool mse = qp.scheme == kMse;
   const float rho = p.rho[0];
   ADMMQ_FIN_STAMP(0);
   const int s32 = (int)start, e32 = (int)end;
@@ -423,10 +445,18 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
     for (int r = threadIdx.x; r < nrows; r += NT) rmax[r] = 0u;
     __syncthreads();
   }
+  if (ADMMQ_TRACE && trace) {
+    __builtin_amdgcn_s_waitcnt(0);
+    ADMMQ_FIN_STAMP(4);
+  }
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
   float4 p4[NG];
   int rows[NG];
+  gf32x4 ho[NG], uo[NG];
   const int lane = threadIdx.x & 63;
+  // every group's arithmetic first, then every store: a store issued between two groups
+  // would be waited for (vmcnt) by the next group's first register read the compiler
+  // cannot prove complete
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
@@ -440,27 +470,31 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
       const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
       const float xs[4] = {ts[0] - us[0], ts[1] - us[1], ts[2] - us[2], ts[3] - us[3]};   // H_T - U
       const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
-      gf32x4 ho, uo, po;
+      float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;   // the group's residual terms (fp32, in order)
+      float po[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (c0 + k < R) {
-          const float hn = apply_quant(xs[k], qp);          // H = quantize(H_T - U)
-          const float dh = hn - ts[k];
-          const float un = us[k] + dh;                      // U += H - H_T
-          ho[k] = hn; uo[k] = un;
-          po[k] = fs[k] + rho * (hn + un);                  // next rhs F + rho(H+U)
-          const float dp = hn - hs[k];
-          s1 += (double)(dh * dh); s2 += (double)(hn * hn);
-          s3 += (double)(dp * dp); s4 += (double)(un * un);
-        } else {
-          ho[k] = 0.f; uo[k] = 0.f; po[k] = 0.f;
-        }
+        const bool ok = c0 + k < R;   // select, not a branch (the pads stay exactly 0)
+        const float hq = mse ? apply_quant_mse(xs[k], qp) : apply_quant(xs[k], qp);   // H = quantize(H_T - U)
+        const float hn = ok ? hq : 0.f;
+        const float dh = ok ? hn - ts[k] : 0.f;
+        const float un = ok ? us[k] + dh : 0.f;              // U += H - H_T
+        ho[g][k] = hn; uo[g][k] = un;
+        po[k] = ok ? fs[k] + rho * (hn + un) : 0.f;          // next rhs F + rho(H+U)
+        const float dp = ok ? hn - hs[k] : 0.f;
+        a1 += dh * dh; a2 += hn * hn; a3 += dp * dp; a4 += un * un;
       }
-      *(gst4*)(Hd + e) = ho;
-      *(gst4*)(Ud + e) = uo;
+      s1 += (double)a1; s2 += (double)a2; s3 += (double)a3; s4 += (double)a4;
       p4[g] = make_float4(po[0], po[1], po[2], po[3]);
-      if (!split) *(gst4*)(Pd + e) = po;
     }
+  }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    if (rows[g] < 0) continue;
+    const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
+    *(gst4*)(Hd + e) = ho[g];
+    *(gst4*)(Ud + e) = uo[g];
+    if (!split) *(gst4*)(Pd + e) = gf32x4{p4[g].x, p4[g].y, p4[g].z, p4[g].w};
   }
   if (split) {   // row max of |next P| per (wave, row): rows are contiguous lane ranges
 #pragma unroll

@@ -59,14 +59,14 @@ for name, j0, j1 in phases:
 starts = sorted((r[0] - t0) / 100 for r in rows)
 print("  start offsets: median %.2f  90%% %.2f  max %.2f us" % (starts[len(starts) // 2], starts[int(0.9 * len(starts))], starts[-1]))
 if fused and hasattr(lib, "admmq_debug_fin_trace"):
-    fb = (ctypes.c_ulonglong * (4 * n))()
+    fb = (ctypes.c_ulonglong * (5 * n))()
     lib.admmq_debug_fin_trace(fb, n)
-    fr = [([fb[4 * b + j] for j in range(4)], rows[b]) for b in range(len(rows))]
+    fr = [([fb[5 * b + j] for j in range(5)], rows[b]) for b in range(len(rows))]
     fr = [(f, r) for f, r in fr if f[0] >= r[4] and f[3] >= f[0]]
     if fr:
         print(f"  finalize sub-phases over {len(fr)} blocks:")
-        for name, a0, a1 in (("start->rho", None, 0), ("elements+stores", 0, 1), ("rowmax barrier", 1, 2),
-                             ("split stores", 2, 3), ("residuals+end", 3, None)):
+        for name, a0, a1 in (("start->rho", None, 0), ("rho->loads done", 0, 4), ("elements+stores", 4, 1),
+                             ("rowmax barrier", 1, 2), ("split stores", 2, 3), ("residuals+end", 3, None)):
             d = [((f[a1] if a1 is not None else r[5]) - (f[a0] if a0 is not None else r[4])) / 100 for f, r in fr]
             print(f"    {name:16s} avg {sum(d)/len(d):6.2f}  max {max(d):6.2f} us")
 sfn = getattr(lib, "admmq_debug_setup_trace", None)

@@ -318,7 +318,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i : order) {   // 128 x 64 tiles (pl.wide, I > 64)
     const ProbDesc& d = pl.desc[i];
     if (!(pl.wide && d.I > 64)) continue;
-    const int TM = d.Ip / 128, TN = (d.ld + 63) / 64;
+    const int TM = d.Ip / 128, TN = (d.ld + 127) / 128;   // 128 x 128 tiles
     for (int g0 = 0; g0 < TN; g0 += 8)
       for (int tm = 0; tm < TM; ++tm)
         for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)

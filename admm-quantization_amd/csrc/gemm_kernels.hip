@@ -92,20 +92,25 @@ __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16
 
 // One workgroup per tile (the grid is the tile list, longest K first, CU-balanced by the
 // planner). SPLIT selects the operand form (see the file header).
-template <int WM, int KS, int NS, bool SPLIT>
+// CW: 32-column sub-tiles per wave (1: BN = 64 columns per tile; 2: 128, each wave's A
+// fragment feeding two sub-tiles - the wide tiles of large launches, CW = 2 with WM = 4:
+// 128 x 128, 8 waves, a third fewer operand bytes per MAC than 128 x 64).
+template <int WM, int KS, int NS, bool SPLIT, int CW = 1>
 __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? (WM == 4 ? 4 : 3) : 1))) void k_gemm(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
-  constexpr int NSUB = 2 * WM;                 // 32 x 32 sub-tiles per workgroup
+  constexpr int BNT = BN * CW;                 // tile columns
+  constexpr int NSUB = 2 * WM;                 // waves per K-slice (each: 32 rows x 32 CW columns)
   constexpr int NW = NSUB * KS;                // waves
   constexpr int NT = 64 * NW;
-  constexpr int ROWS = BM + BN;                // image rows per stage (A then B)
+  constexpr int ROWS = BM + BNT;               // image rows per stage (A then B)
   constexpr int STAGE = ROWS * 32;             // floats per stage
   constexpr int NG = ROWS / 8;                 // glds wave-instructions per stage (8 rows each)
   constexpr int GPW = NG / NW;                 // ... per wave
   constexpr int QS = 4 / KS;                   // fp32: b128 fragment reads per operand per wave per K-step
   constexpr int KCW = 2 / KS;                  // split: 16-deep k chunks per wave per K-step
   static_assert(KS == 1 || (KS - 1) * NSUB * 1024 <= STAGE, "split-K partials fit in one stage");
+  static_assert(CW == 1 || (CW == 2 && KS == 1), "CW");
   static_assert(NG % NW == 0, "stage rows must split evenly over the waves");
   static_assert(KS == 1 || KS == 2 || (!SPLIT && KS == 4), "KS");
   static_assert(NS >= 2 && NS <= 4 && GPW * (NS - 2) < 64, "NS");
@@ -126,12 +131,12 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   const int wm = sub / 2, wn = sub & 1;
   const int i = lane & 31, h = lane >> 5;
   const int swz = (i >> 1) & 7;
-  const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * wn + i) * 32;
+  const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * CW * wn + i) * 32;   // sub-tile c: boff + 32 * 32 c
 
   const GemmTile tl = tiles[blockIdx.x];
   const ProbDesc& p = probs[tl.prob];
   const int ld = tl.ld, ldm = tl.ldm;
-  const int row0 = tl.tm * BM, col0 = tl.tn * BN;
+  const int row0 = tl.tm * BM, col0 = tl.tn * BNT;
   const int nk = tl.nk;
   // the epilogue's U entries (X = H_T - U) and, split form, the row / column exponents:
   // loaded before the first stages so their latency is spent under the K-loop (vector
@@ -139,19 +144,22 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   // (wide tiles, WM = 4: loaded in the epilogue instead - those launches run many rounds
   // of tiles, so other workgroups cover the latency, and the registers stay free)
   constexpr bool PRE = WM < 4;
-  float upre[16];
+  float upre[CW][16];
   int epre[16];
-  int ecol = 0;
+  int ecol[CW] = {};
   auto load_epi = [&]() {
-    const int col = col0 + 32 * wn + i;
-    const int colc = col < ld ? col : 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-      upre[r] = ldg(tl.U + (size_t)row * ld + colc);
-      if (SPLIT) epre[r] = *(__attribute__((address_space(1))) const int*)(tl.eP + row);
+    for (int c = 0; c < CW; ++c) {
+      const int col = col0 + 32 * (CW * wn + c) + i;
+      const int colc = col < ld ? col : 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+        upre[c][r] = ldg(tl.U + (size_t)row * ld + colc);
+        if (SPLIT && c == 0) epre[r] = *(__attribute__((address_space(1))) const int*)(tl.eP + row);
+      }
+      if (SPLIT) ecol[c] = *(__attribute__((address_space(1))) const int*)(tl.eM + colc);
     }
-    if (SPLIT) ecol = *(__attribute__((address_space(1))) const int*)(tl.eM + colc);
   };
   if constexpr (PRE) load_epi();
   // per-lane global source of each of this wave's glds pieces (K-step 0)
@@ -161,8 +169,10 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
     const int g = wave * GPW + j;
     const int r = 8 * g + (lane >> 3);                       // image row
     const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+    // B rows past ldm (the last 128-column tile of a CW = 2 launch) read the last row: they
+    // only feed columns >= ld, which are never stored
     src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + 4 * c
-                      : tl.M + (size_t)(col0 + r - BM) * ldm + 4 * c;
+                      : tl.M + (size_t)min(col0 + r - BM, ldm - 1) * ldm + 4 * c;
   }
 #define ADMMQ_ISSUE(s, kt)                                                 \
   _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
@@ -189,9 +199,11 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
     if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
   }
 
-  f32x16 acc;
+  f32x16 acc[CW];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int c = 0; c < CW; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
 
   // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
   // stages stay in flight), publish it (barrier), refill the stage consumed one step
@@ -213,21 +225,25 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
         const int ch = ((2 * kc + h) ^ swz) * 4, cl = ((4 + 2 * kc + h) ^ swz) * 4;           \
         const f16x8 ah = as_h8(*reinterpret_cast<const float4*>(st + aoff + ch));             \
         const f16x8 al = as_h8(*reinterpret_cast<const float4*>(st + aoff + cl));             \
-        const f16x8 bh = as_h8(*reinterpret_cast<const float4*>(st + boff + ch));             \
-        const f16x8 bl = as_h8(*reinterpret_cast<const float4*>(st + boff + cl));             \
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);                   \
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);                   \
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);                   \
+        _Pragma("unroll") for (int c = 0; c < CW; ++c) {                                      \
+          const f16x8 bh = as_h8(*reinterpret_cast<const float4*>(st + boff + 1024 * c + ch)); \
+          const f16x8 bl = as_h8(*reinterpret_cast<const float4*>(st + boff + 1024 * c + cl)); \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[c], 0, 0, 0);           \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[c], 0, 0, 0);           \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[c], 0, 0, 0);           \
+        }                                                                                     \
       }                                                                                       \
     } else {                                                                                  \
       _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                     \
         const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                                  \
         const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);                  \
-        const float4 b = *reinterpret_cast<const float4*>(st + boff + cpos);                  \
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);                   \
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);                   \
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);                   \
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);                   \
+        _Pragma("unroll") for (int c = 0; c < CW; ++c) {                                      \
+          const float4 b = *reinterpret_cast<const float4*>(st + boff + 1024 * c + cpos);     \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[c], 0, 0, 0);           \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[c], 0, 0, 0);           \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[c], 0, 0, 0);           \
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[c], 0, 0, 0);           \
+        }                                                                                     \
       }                                                                                       \
     }                                                                                         \
   } while (0)
@@ -246,7 +262,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
     if (ks > 0) {
       float* dst = st0 + ((ks - 1) * NSUB + sub) * 1024;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
+      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[0][r];
     }
     __syncthreads();
     if (ks == 0) {
@@ -254,7 +270,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
       for (int j = 1; j < KS; ++j) {
         const float* s2 = st0 + ((j - 1) * NSUB + sub) * 1024;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += s2[r * 64 + lane];
+        for (int r = 0; r < 16; ++r) acc[0][r] += s2[r * 64 + lane];
       }
     }
   }
@@ -262,27 +278,30 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   if (ks == 0) {
     if constexpr (!PRE) load_epi();
-    const int col = col0 + 32 * wn + i;
     unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
     // descriptor fields once into registers (the stores below may alias the descriptor)
     typedef __attribute__((address_space(1))) float gf32;
     gf32* const HTg = (gf32*)p.HT;
     gf32* const Xg = p.X_dbg ? (gf32*)p.X : nullptr;   // X = H_T - U is re-formed by its readers; debug output only
     const int pI = p.I, pR = p.R;
-    if (col < ld) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const size_t off = (size_t)row * ld + col;
-        const float ht = SPLIT ? __builtin_ldexpf(acc[r], -(epre[r] + ecol)) : acc[r];
-        const float x = ht - upre[r];
-        HTg[off] = ht;
-        if (Xg) Xg[off] = x;
-        if (row < pI && col < pR) {
-          amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
-          const unsigned e = enc_ord(x);
-          mn = min(mn, e);
-          mxo = max(mxo, e);
+    for (int c = 0; c < CW; ++c) {
+      const int col = col0 + 32 * (CW * wn + c) + i;
+      if (col < ld) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const size_t off = (size_t)row * ld + col;
+          const float ht = SPLIT ? __builtin_ldexpf(acc[c][r], -(epre[r] + ecol[c])) : acc[c][r];
+          const float x = ht - upre[c][r];
+          HTg[off] = ht;
+          if (Xg) Xg[off] = x;
+          if (row < pI && col < pR) {
+            amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
+            const unsigned e = enc_ord(x);
+            mn = min(mn, e);
+            mxo = max(mxo, e);
+          }
         }
       }
     }
@@ -548,7 +567,7 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s) {
-  // tiles[0 .. ntiles_wide) are 128x64 (WM = 4: eight waves, one per 32x32 sub-tile, the
+  // tiles[0 .. ntiles_wide) are 128x128 (WM = 4, CW = 2: eight waves of 32 x 64, the
   // launches with many rounds of tiles), then ntiles_big 64x64 tiles (WM = 2, four
   // waves, 3-deep ring), then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors,
   // 2 waves per sub-tile splitting each K-step, 4-deep ring)
@@ -559,7 +578,12 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
     else                                                                                                             \
       hipLaunchKernelGGL((k_gemm<WM, KS, NS, false>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
   } while (0)
-  if (ntiles_wide > 0) ADMMQ_GEMM(4, 1, 3, ntiles_wide, tiles);
+  if (ntiles_wide > 0) {   // 128 x 128 tiles (CW = 2), four-deep ring, one workgroup per CU
+    if (split)
+      hipLaunchKernelGGL((k_gemm<4, 1, 4, true, 2>), dim3(ntiles_wide), dim3(512), 0, s, d, tiles, slot, iter, eps, ncand);
+    else
+      hipLaunchKernelGGL((k_gemm<4, 1, 4, false, 2>), dim3(ntiles_wide), dim3(512), 0, s, d, tiles, slot, iter, eps, ncand);
+  }
   if (ntiles_big > 0) ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
   if (ntiles_small > 0) ADMMQ_GEMM(1, 2, 4, ntiles_small, tiles + ntiles_wide + ntiles_big);
 #undef ADMMQ_GEMM

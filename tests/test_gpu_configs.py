@@ -163,8 +163,9 @@ def test_c5_llama_shapes(torch_dev, I, J, R, solve):
 
 
 def test_wide_tiles_equal_64x64(torch_dev):
-    """The 128x64 tiles (a launch with >= kWideMinTiles 64x64 tiles, e.g. the Llama MLP
-    factor) compute each element with the same K order as the 64x64 tiles: a (512, 1141)
+    """The 128x128 tiles (a launch with >= kWideMinTiles 64x64 tiles, e.g. the Llama MLP
+    factor; two 32-column sub-tiles per wave) compute each element with the same K order
+    and MFMA sequence as the 64x64 tiles: a (512, 1141)
     factor solved beside an (11008, 1492) one (wide tiles) equals the same factor solved
     alone (64x64 tiles) bit for bit, over 3 inner iterations, in both solve forms."""
     torch, dev = torch_dev

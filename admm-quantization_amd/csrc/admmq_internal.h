@@ -38,7 +38,8 @@ constexpr int kResRep = 8;         // replicas of the per-problem residual sums 
 constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU split-K solve
 constexpr int kThinCols = 256;     // ... columns per unit (64 lanes x float4)
 constexpr int kThinK = 128;        // ... reduction rows per unit (4 waves x 32)
-constexpr long long kWideMinTiles = 4 * 768;   // 64x64 tiles of a launch from which I > 64 factors take 128x64 tiles
+constexpr long long kWideMinTiles = 4 * 768;   // 64x64 tiles of a launch from which I > 64 factors take wide tiles
+constexpr int kWideRows = 256;                 // ... of kWideRows x 128 (k_gemm<8, 1, 3, *, 2>)
 
 // Quantizer state of one job (an ADMM problem's X, or a standalone tensor), with
 // `nslot` parity slots. The MSE-minmax search (source/quantization.py:118-144) runs in

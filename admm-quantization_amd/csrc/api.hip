@@ -272,7 +272,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? 128 : 64);
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? kWideRows : 64);
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -318,7 +318,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i : order) {   // 128 x 64 tiles (pl.wide, I > 64)
     const ProbDesc& d = pl.desc[i];
     if (!(pl.wide && d.I > 64)) continue;
-    const int TM = d.Ip / 128, TN = (d.ld + 127) / 128;   // 128 x 128 tiles
+    const int TM = d.Ip / kWideRows, TN = (d.ld + 127) / 128;   // kWideRows x 128 tiles
     for (int g0 = 0; g0 < TN; g0 += 8)
       for (int tm = 0; tm < TM; ++tm)
         for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)

@@ -96,7 +96,7 @@ __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16
 // fragment feeding two sub-tiles - the wide tiles of large launches, CW = 2 with WM = 4:
 // 128 x 128, 8 waves, a third fewer operand bytes per MAC than 128 x 64).
 template <int WM, int KS, int NS, bool SPLIT, int CW = 1>
-__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(NS <= 3 ? (WM == 4 ? 4 : 3) : 1))) void k_gemm(
+__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(WM == 8 ? 4 : (NS <= 3 ? (WM == 4 ? 4 : 3) : 1)))) void k_gemm(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
   constexpr int BNT = BN * CW;                 // tile columns
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(N
   // loads complete in issue order: the stage waits below then also cover these)
   // (wide tiles, WM = 4: loaded in the epilogue instead - those launches run many rounds
   // of tiles, so other workgroups cover the latency, and the registers stay free)
-  constexpr bool PRE = WM < 4;
+  constexpr bool PRE = WM < 4;   // (WM >= 4: the epilogue loads after the K-loop)
   float upre[CW][16];
   int epre[16];
   int ecol[CW] = {};
@@ -578,11 +578,11 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
     else                                                                                                             \
       hipLaunchKernelGGL((k_gemm<WM, KS, NS, false>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
   } while (0)
-  if (ntiles_wide > 0) {   // 128 x 128 tiles (CW = 2), four-deep ring, one workgroup per CU
+  if (ntiles_wide > 0) {   // 256 x 128 tiles (WM = 8, CW = 2: 16 waves of 32 x 64), three-deep ring, one workgroup per CU
     if (split)
-      hipLaunchKernelGGL((k_gemm<4, 1, 4, true, 2>), dim3(ntiles_wide), dim3(512), 0, s, d, tiles, slot, iter, eps, ncand);
+      hipLaunchKernelGGL((k_gemm<8, 1, 3, true, 2>), dim3(ntiles_wide), dim3(1024), 0, s, d, tiles, slot, iter, eps, ncand);
     else
-      hipLaunchKernelGGL((k_gemm<4, 1, 4, false, 2>), dim3(ntiles_wide), dim3(512), 0, s, d, tiles, slot, iter, eps, ncand);
+      hipLaunchKernelGGL((k_gemm<8, 1, 3, false, 2>), dim3(ntiles_wide), dim3(1024), 0, s, d, tiles, slot, iter, eps, ncand);
   }
   if (ntiles_big > 0) ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
   if (ntiles_small > 0) ADMMQ_GEMM(1, 2, 4, ntiles_small, tiles + ntiles_wide + ntiles_big);

@@ -167,8 +167,8 @@ struct AdmmPlan {
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
-  int ntiles_wide = 0, ntiles_big = 0, ntiles_small = 0;   // 128x64, 64x64, 32x64 tiles (in that order)
-  bool wide = false;                                       // I > 64 factors take 128x64 tiles (k_gemm<4, ..>)
+  int ntiles_wide = 0, ntiles_big = 0, ntiles_small = 0;   // 256x128, 64x64, 32x64 tiles (in that order)
+  bool wide = false;                                       // I > 64 factors take 256x128 tiles (k_gemm<8, 1, 3, *, 2>)
   int fin_groups = 1;             // float4 groups per thread of the finalize units
   int hist_nv = 1;
   std::vector<int> small;         // jobs with I <= kThinRows (one-block fused search + finalize)
@@ -252,7 +252,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.split = g_solve_mode.load() == kSolveSplit;
   // Wide tiles when the 64x64 tiles would take many rounds of the resident slots
   // (256 CUs x 3): then a CU's bytes per MAC matter more than the number of tiles, and
-  // 128x64 tiles read 3/4 of the operand bytes per MAC (the Llama shapes of C5). The
+  // 256x128 tiles read 3/8 of the operand bytes per MAC (the Llama shapes of C5). The
   // element results do not depend on the tile shape (same K order per element).
   {
     long long t64 = 0;

@@ -567,7 +567,7 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s) {
-  // tiles[0 .. ntiles_wide) are 128x128 (WM = 4, CW = 2: eight waves of 32 x 64, the
+  // tiles[0 .. ntiles_wide) are 256x128 (WM = 8, CW = 2: sixteen waves of 32 x 64, the
   // launches with many rounds of tiles), then ntiles_big 64x64 tiles (WM = 2, four
   // waves, 3-deep ring), then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors,
   // 2 waves per sub-tile splitting each K-step, 4-deep ring)

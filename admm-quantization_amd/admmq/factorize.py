@@ -20,6 +20,7 @@ loop; the intended 4-D -> 3-D reshape of ``:140-147`` is applied
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import time
 from dataclasses import dataclass, field
@@ -77,7 +78,9 @@ class LayerRun:
 
 def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: int, qscheme: str,
               num_attempts: int = 200, record_errors: bool = True, tol: float = 1e-5):
-    """One ALS sweep over all active layers (modes batched across layers)."""
+    """One ALS sweep over all active layers (modes batched across layers). Returns the
+    factor-iterations the inner ADMM loops ran in this sweep, per active layer
+    (``{id(run): count}``)."""
     act = [r for r in runs if r.active]
     nmodes = max((len(r.factors) for r in act), default=0)
     infos = []
@@ -88,16 +91,23 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
         # no per-call sync for the SPD test: the flags are read once per sweep (below)
         Hs, info = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
                                           check_spd=False, return_info=True)
-        infos.append(info[:, 2])
+        infos.append(info[:, [0, 2]])   # {iterations run, spd_error}
         for r, H in zip(sel, Hs):
             r.factors[mode] = H
         qs = quantize_batched(Hs, bits, qscheme, num_attempts=num_attempts)
         for r, q in zip(sel, qs):
             r.quantized[mode] = q
+    iters = {id(r): 0 for r in act}
     if infos:
-        check_spd_flags(infos, act, nmodes)
+        both = torch.cat(infos).cpu()   # the sweep's one host sync for the flags
+        check_spd_flags([both[:, 1]], act, nmodes)
+        k = 0
+        for mode in range(nmodes):
+            for r in (r for r in act if mode < len(r.factors)):
+                iters[id(r)] += int(both[k, 0])
+                k += 1
     if not record_errors:
-        return
+        return iters
     errs = rel_error_batched([(r.W, r.factors) for r in act] + [(r.W, r.quantized) for r in act])
     for n, r in enumerate(act):
         r.loss.append(errs[n])
@@ -109,6 +119,7 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
             r.active = False
         else:   # the 2-way script's end-of-body assignment (scripts/factorize.py:309-310)
             r.saved, r.saved_quantized = list(r.factors), list(r.quantized)
+    return iters
 
 
 def check_spd_flags(infos, runs, nmodes):
@@ -130,8 +141,13 @@ def check_spd_flags(infos, runs, nmodes):
 def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_iter_als: int, max_iter_admm: int,
                      bits: int = 4, qscheme: str = "tensor_mseminmax_symmetric", init: str = "random", seed: int = 42,
                      names: Optional[Sequence[str]] = None, eps: float = 1e-8, tol: float = 1e-5,
-                     num_attempts: int = 200, initial_factors=None) -> List[LayerRun]:
-    """``--method admm`` of scripts/factorize.py for a batch of layers."""
+                     num_attempts: int = 200, initial_factors=None, metrics=None) -> List[LayerRun]:
+    """``--method admm`` of scripts/factorize.py for a batch of layers.
+
+    ``metrics``: optional callable receiving one dict per (sweep, layer) - the keys the
+    reference logs to wandb per ALS iteration (``rec_error``, ``quant_rec_error``,
+    scripts/factorize.py:249-253, 301-305) plus the sweep's wall time and ADMM
+    factor-iterations (see :func:`sweep_records`)."""
     runs = []
     for i, (W, R) in enumerate(zip(weights, ranks)):
         fs = initial_factors[i] if initial_factors is not None else init_factors(W, rank=R, init=init, device=W.device,
@@ -145,11 +161,51 @@ def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_
             run.lossq.append(eq)
             run.saved_quantized = list(q)
         runs.append(run)
-    for _ in range(max_iter_als):
+    for sweep in range(max_iter_als):
         if not any(r.active for r in runs):
             break
-        als_sweep(runs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts, tol=tol)
+        act = [r for r in runs if r.active]
+        t0 = time.perf_counter()
+        iters = als_sweep(runs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts, tol=tol)
+        dt = time.perf_counter() - t0   # the errors above were read on the host: the sweep is complete
+        if metrics is not None:
+            for rec in sweep_records(act, sweep, iters, dt):
+                metrics(rec)
     return runs
+
+
+def sweep_records(runs: Sequence[LayerRun], sweep: int, iters: dict, seconds: float) -> List[dict]:
+    """JSONL metric records of one ALS sweep (the reference prints / logs
+    to wandb; this build writes one JSON object per (sweep, layer)). ``sweep_s`` and
+    ``factor_iterations_per_s`` are for the whole batched sweep (all layers share its
+    launches); ``factor_iterations`` is the layer's own inner-iteration count."""
+    total = sum(iters.values())
+    out = []
+    for r in runs:
+        out.append({"sweep": sweep, "layer": r.name, "rank": r.rank,
+                    "rec_error": r.loss[-1] if r.loss else None,
+                    "quant_rec_error": r.lossq[-1] if r.lossq else None,
+                    "factor_iterations": int(iters.get(id(r), 0)), "active": bool(r.active),
+                    "sweep_s": seconds, "factor_iterations_per_s": (total / seconds) if seconds > 0 else None})
+    return out
+
+
+class JsonlWriter:
+    """Appends one JSON object per line to ``path`` (flushed per record)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        self._f = open(path, "a")
+
+    def __call__(self, rec: dict):
+        self._f.write(json.dumps(rec) + "\n")
+        self._f.flush()
+
+    def close(self):
+        self._f.close()
 
 
 def _layer_weight(args, device):
@@ -169,7 +225,9 @@ def _layer_weight(args, device):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description="ADMM quantized CP factorization of one layer (MI355X)")
     ap.add_argument("--model-name", type=str, required=True, help="[resnet18, resnet50, llama7b]")
-    ap.add_argument("--with-wandb", action="store_true", help="accepted for compatibility; logging is JSONL")
+    ap.add_argument("--with-wandb", action="store_true",
+                    help="log per-sweep metrics (JSONL at <outdir>/<prefix>_metrics.jsonl unless --metrics-jsonl)")
+    ap.add_argument("--metrics-jsonl", type=str, default=None, help="per-sweep JSONL metrics file")
     ap.add_argument("--method", type=str, required=True, help="[admm, parafac, parafac-epc]")
     ap.add_argument("--init", type=str, default="random", help="[random, svd, parafac, parafac-epc]")
     ap.add_argument("--layer", type=str, required=True)
@@ -204,9 +262,15 @@ def main(argv=None):
     os.makedirs(outdir, exist_ok=True)
     fileprefix = f'{args.layer}_{args.method}_{args.init}_rank_{args.rank}'
     start = time.time()
+    mpath = args.metrics_jsonl or (os.path.join(outdir, fileprefix + '_metrics.jsonl') if args.with_wandb else None)
+    writer = JsonlWriter(mpath) if mpath else None
     if args.method == 'admm':
-        run = factorize_layers([weight], [args.rank], args.max_iter_als, args.max_iter_admm, args.bits, args.qscheme,
-                               args.init, args.seed, names=[args.layer])[0]
+        try:
+            run = factorize_layers([weight], [args.rank], args.max_iter_als, args.max_iter_admm, args.bits,
+                                   args.qscheme, args.init, args.seed, names=[args.layer], metrics=writer)[0]
+        finally:
+            if writer is not None:
+                writer.close()
         factors, factors_q = run.result()
         torch.save(run.loss, os.path.join(outdir, fileprefix + '_losshist.pt'))
         torch.save(run.lossq, os.path.join(outdir, fileprefix + '_lossquanthist.pt'))

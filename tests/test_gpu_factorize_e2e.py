@@ -10,6 +10,7 @@ loss histories as Python float lists, the saved factors equal to the driver's re
 the calibrate-side load + admmq.export.build_cp_layer / build_cp2conv_layer reproducing the
 CP reconstruction as a convolution (source/models.py:24-74).
 """
+import json
 import os
 
 import pytest
@@ -37,7 +38,7 @@ def test_factorize_cli_outputs(tmp_path, model, layer, three_way):
     from admmq.export import build_cp_layer, build_cp2conv_layer
     argv = ["--model-name", model, "--method", "admm", "--layer", layer, "--reduction-rate", "2.0", "--bits", "4",
             "--seed", "42", "--qscheme", "tensor_mseminmax_symmetric", "--max_iter_als", "3", "--max_iter_admm", "20",
-            "--outdir-root", str(tmp_path)]
+            "--outdir-root", str(tmp_path), "--metrics-jsonl", str(tmp_path / "metrics.jsonl")]
     factors, factors_q = factorize.main(argv)
     idx, spec = synthetic.find_layer(model, layer)
     W = torch.from_numpy(synthetic.layer_weight(spec, idx))
@@ -58,6 +59,11 @@ def test_factorize_cli_outputs(tmp_path, model, layer, three_way):
     lq = torch.load(out / f"{prefix}_lossquanthist.pt", weights_only=True)
     assert isinstance(lh, list) and all(isinstance(v, float) for v in lh) and 1 <= len(lh) <= 3
     assert len(lq) == len(lh) and all(0.0 < v < 1.5 for v in lh + lq)
+    # SURVEY §5 metrics: one JSONL record per sweep, the errors equal the saved histories
+    recs = [json.loads(x) for x in (tmp_path / "metrics.jsonl").read_text().splitlines()]
+    assert [r["sweep"] for r in recs] == list(range(len(lh)))
+    assert [r["rec_error"] for r in recs] == lh and [r["quant_rec_error"] for r in recs] == lq
+    assert all(r["layer"] == layer and 0 < r["factor_iterations"] <= 20 * W.dim() and r["sweep_s"] > 0 for r in recs)
     # the calibrate side: the CP layer built from the files equals the CP reconstruction
     cout, cin = W.shape[0], W.shape[1]
     if three_way:

@@ -103,3 +103,29 @@ def test_torch_port_vs_reference_fixtures():
         H, U = torch_port.admm_iteration(H0, torch.zeros_like(H0), F, G, 2, 1e-8, 4)
         ref = z[f"l1_m{mode}_tensor_mseminmax_symmetric_it2_U"]
         assert np.linalg.norm(U.numpy() - ref) / np.linalg.norm(ref) < 1e-5
+
+
+def test_sweep_metrics_jsonl(tmp_path):
+    """SURVEY §5 metrics: one JSON object per (sweep, layer) with the reference's wandb keys
+    (scripts/factorize.py:249-253) plus the sweep's wall time and factor-iterations."""
+    from admmq.factorize import JsonlWriter, LayerRun, parse_args, sweep_records
+    runs = [LayerRun("a", torch.zeros(4, 3, 9), 2, [torch.zeros(4, 2), torch.zeros(3, 2), torch.zeros(9, 2)]),
+            LayerRun("b", torch.zeros(5, 6), 3, [torch.zeros(5, 3), torch.zeros(6, 3)])]
+    runs[0].loss, runs[0].lossq = [0.5, 0.4], [0.6, 0.45]
+    runs[1].loss, runs[1].lossq = [0.3], [0.35]
+    runs[1].active = False
+    iters = {id(runs[0]): 3 * 999, id(runs[1]): 2 * 17}
+    recs = sweep_records(runs, 1, iters, 2.0)
+    w = JsonlWriter(str(tmp_path / "sub" / "m.jsonl"))
+    for r in recs:
+        w(r)
+    w.close()
+    back = [json.loads(x) for x in (tmp_path / "sub" / "m.jsonl").read_text().splitlines()]
+    assert back == recs
+    assert [r["layer"] for r in back] == ["a", "b"] and all(r["sweep"] == 1 for r in back)
+    assert back[0]["rec_error"] == 0.4 and back[0]["quant_rec_error"] == 0.45 and back[0]["factor_iterations"] == 2997
+    assert back[1]["active"] is False and back[1]["factor_iterations"] == 34
+    assert back[0]["factor_iterations_per_s"] == pytest.approx((2997 + 34) / 2.0)
+    a = parse_args(["--model-name", "resnet18", "--method", "admm", "--layer", "layer1.0.conv1", "--rank", "8",
+                    "--bits", "4", "--seed", "0", "--qscheme", "tensor_minmax_symmetric", "--with-wandb"])
+    assert a.with_wandb and a.metrics_jsonl is None

@@ -314,15 +314,44 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   std::vector<int> order(nprob);
   for (int i = 0; i < nprob; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pl.desc[a].ld > pl.desc[b].ld; });
+  // Wide tiles (kWideRows x 128, pl.wide, I > 64), placed by XCD: workgroup b runs on XCD
+  // b mod 8, in order of b within the XCD. These launches have I >> R (the Llama shapes),
+  // so the P row panel (kWideRows x ld) is the big operand: every row panel goes to ONE
+  // XCD (least K-step load first), which runs all of its column tiles back to back, so P is
+  // fetched once into that XCD's L2 instead of once per XCD (the column-major order kept
+  // a column tile of M per XCD and made all 8 XCDs fetch every P panel: 3.5x the
+  // algorithmic bytes at C5). Queue x fills positions x, x + 8, ...; a queue that runs
+  // out early takes tiles from the tail of the longest one.
   std::vector<GemmTile> wide;
-  for (int i : order) {   // 128 x 64 tiles (pl.wide, I > 64)
-    const ProbDesc& d = pl.desc[i];
-    if (!(pl.wide && d.I > 64)) continue;
-    const int TM = d.Ip / kWideRows, TN = (d.ld + 127) / 128;   // kWideRows x 128 tiles
-    for (int g0 = 0; g0 < TN; g0 += 8)
-      for (int tm = 0; tm < TM; ++tm)
-        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
-          wide.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+  {
+    constexpr int kXcd = 8;
+    std::vector<std::vector<GemmTile>> q(kXcd);
+    std::vector<long long> qload(kXcd, 0);
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if (!(pl.wide && d.I > 64)) continue;
+      const int TM = d.Ip / kWideRows, TN = (d.ld + 127) / 128;
+      for (int tm = 0; tm < TM; ++tm) {
+        const int x = (int)(std::min_element(qload.begin(), qload.end()) - qload.begin());
+        for (int tn = 0; tn < TN; ++tn) q[x].push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+        qload[x] += (long long)TN * (d.ld / 32);
+      }
+    }
+    std::vector<size_t> head(kXcd, 0);
+    size_t left = 0;
+    for (auto& v : q) left += v.size();
+    for (size_t b = 0; left > 0; ++b, --left) {
+      int x = (int)(b % kXcd);
+      if (head[x] >= q[x].size()) {   // exhausted: the longest remaining queue donates its last tile
+        int y = 0;
+        for (int z = 1; z < kXcd; ++z)
+          if (q[z].size() - head[z] > q[y].size() - head[y]) y = z;
+        wide.push_back(q[y].back());
+        q[y].pop_back();
+        continue;
+      }
+      wide.push_back(q[x][head[x]++]);
+    }
   }
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];

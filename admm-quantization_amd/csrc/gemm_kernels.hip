@@ -478,16 +478,21 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
     v[r] = a;
   }
   if (u.nkg > 1) {
-    float* part = p.Part + (size_t)u.kg * NR * ld;
+    // The partial slab is handed over write-through (16-B sc1 buffer stores, drained
+    // before the counter add) and read back by the last block with sc1 buffer loads only,
+    // so no agent-scope acquire (an L1 invalidate, ~1.7 us on the last block's path) is
+    // needed (cdna_hip_programming.md Guideline 16, sc1 consumer).
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(p.Part, 0, (int)((size_t)u.nkg * NR * ld * sizeof(float)), 0x00020000);
     if (cok) {
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         if (wave + 4 * r >= NR) continue;
-        float* d = part + (size_t)(wave + 4 * r) * ld + col;
-        __hip_atomic_store(d + 0, v[r].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 1, v[r].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 2, v[r].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 3, v[r].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int off = (int)((((size_t)u.kg * NR + wave + 4 * r) * ld + col) * sizeof(float));
+        const u32x4 w = {__float_as_uint(v[r].x), __float_as_uint(v[r].y), __float_as_uint(v[r].z),
+                         __float_as_uint(v[r].w)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, prs, off, 0, 16);   // aux 16: sc1 (write-through)
       }
     }
     __builtin_amdgcn_s_waitcnt(0);   // this thread's partial stores are complete
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
     }
     __syncthreads();
     if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' partials are visible
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // only keeps the sc1 loads below the ticket
     // sum the nkg partials in kg order, 8 reduction blocks' loads in flight at a time
 #pragma unroll
     for (int r = 0; r < RW; ++r) v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -511,8 +516,11 @@ __global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ 
       for (int gg = 0; gg < 8; ++gg) {
         const int g = min(g0 + gg, u.nkg - 1);
 #pragma unroll
-        for (int r = 0; r < RW; ++r)
-          t[gg][r] = ldg4(p.Part + ((size_t)g * NR + min(wave + 4 * r, NR - 1)) * ld + cc);
+        for (int r = 0; r < RW; ++r) {
+          const int off = (int)((((size_t)g * NR + min(wave + 4 * r, NR - 1)) * ld + cc) * sizeof(float));
+          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 16);   // sc1
+          t[gg][r] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
+        }
       }
 #pragma unroll
       for (int gg = 0; gg < 8; ++gg) {

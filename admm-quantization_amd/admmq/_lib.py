@@ -94,6 +94,7 @@ def load() -> ctypes.CDLL:
         "admmq_debug_admm_plan_bytes": (S, [P, I32, I32, P]),
         "admmq_debug_check_thresholds": (I32, [ctypes.c_uint32, I32]),
         "admmq_debug_set_fused_finalize": (I32, [I32]),
+        "admmq_debug_set_search_units_per_block": (I32, [I32]),
         "admmq_debug_check_cells": (I32, [I32, I32, ctypes.c_uint32, I32, P]),
         "admmq_profile_begin": (I32, [I32, I32]),
         "admmq_profile_end": (I32, [P, P]),
@@ -208,6 +209,23 @@ class fused_finalize:
 
     def __exit__(self, *exc):
         load().admmq_debug_set_fused_finalize(1)
+        return False
+
+
+class search_units_per_block:
+    """Context manager: stage-1 units per block of the search launch that runs without the
+    fused finalize (0 = the planner's choice). Same integers for any value; used as a
+    cross-check in the parity tests. Restores the planner's choice on exit."""
+
+    def __init__(self, reps: int):
+        self.reps = reps
+
+    def __enter__(self):
+        check(load().admmq_debug_set_search_units_per_block(int(self.reps)), "search_units_per_block")
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_search_units_per_block(0)
         return False
 
 

@@ -131,6 +131,11 @@ struct Chunk {
   const float* H;   // ADMM finalize units: the current H and the padded F
   const float* F;
   const int* sel;   // ADMM finalize units: the job's search record [slot][2 + kMaxSel]
+  // k_mse_hist3 without the fused finalize: `reps` consecutive stage-1 units of `step`
+  // elements in one block (one table setup and one histogram flush for all of them;
+  // `total` is then the last unit's end); `nblk` = blocks of this job in the launch
+  // (the ticket count). 0 = one unit / the job's nhist.
+  int reps, step, nblk, pad2_;
 };
 
 // Loads through global (not flat) pointers: flat loads also count in lgkmcnt, and a
@@ -217,6 +222,8 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
 constexpr int kHistElems = 4096;    // elements per stage-1 work unit x hist_nv (1024 x 4 legacy, 512 x 8 merged)
+constexpr int kHistMultiRounds = 3;   // non-fused search: units per block sized for ~3 rounds of kHistMaxUnits blocks
+constexpr int kHistMultiMaxReps = 8;  // ... at most 8 units per block
 constexpr int kHistMaxUnits = 512;  // stage-1 units that fit in one round (2 per CU): above, 2x larger units
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
 constexpr int kFinElems = 4096;     // elements per ADMM finalize work unit when there are >= kFinMinUnits of them

@@ -68,6 +68,8 @@ static std::atomic<int> g_solve_mode{kSolveSplit};
 // fused finalize (k_mse_hist3<.., true>) where the residency check allows it; 0: the
 // separate k_finalize_admm launch (A/B and cross-check, same integers)
 static std::atomic<bool> g_fused_finalize{true};
+// stage-1 units per block of the non-fused search launch (0: sized by the planner)
+static std::atomic<int> g_hist_reps{0};
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
@@ -153,6 +155,9 @@ struct AdmmPlan {
   std::vector<ProbDesc> desc;
   std::vector<GemmTile> tiles;
   std::vector<Chunk> sse_chunks, fin_chunks, hist_chunks;
+  std::vector<Chunk> hist_multi;   // the same units, several per block (launches without the fused finalize)
+  Chunk* d_hist_multi = nullptr;
+  int nhm_big = 0;                 // hist_multi blocks of the big jobs (listed first)
   ProbDesc* d_desc = nullptr;
   GemmTile* d_tiles = nullptr;
   Chunk* d_sse = nullptr;
@@ -428,6 +433,35 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     }
     if (pass == 0) { pl.nfin_big = (int)pl.fin_chunks.size(); pl.nhist_big = (int)pl.hist_chunks.size(); }
   }
+  // Without the fused finalize (the search launch cannot hold every unit at once, e.g.
+  // C5: ~6800 units) every block repeats the table setup (~6 us) and the histogram flush
+  // for one 8192-element unit; instead a block takes `reps` consecutive units of its job,
+  // sized for about kHistMultiRounds rounds of resident blocks.
+  pl.hist_multi.clear();
+  pl.nhm_big = 0;
+  {
+    const long long nu_all = (long long)pl.hist_chunks.size();
+    const int forced = g_hist_reps.load();
+    const int reps = forced > 0 ? forced
+                                : (int)std::max(1LL, std::min<long long>(kHistMultiMaxReps,
+                                                                         nu_all / (kHistMultiRounds * kHistMaxUnits)));
+    for (size_t a = 0; a < pl.hist_chunks.size();) {
+      size_t b = a;   // the job's units are contiguous
+      while (b < pl.hist_chunks.size() && pl.hist_chunks[b].job == pl.hist_chunks[a].job) ++b;
+      const int nblk = (int)((b - a + reps - 1) / reps);
+      for (size_t c = a; c < b; c += reps) {
+        const size_t e = std::min(b, c + reps) - 1;
+        Chunk k = pl.hist_chunks[c];
+        k.reps = (int)(e - c + 1);
+        k.step = (int)(pl.hist_chunks[c].total - pl.hist_chunks[c].start);   // a full unit unless it is the last
+        k.total = pl.hist_chunks[e].total;
+        k.nblk = nblk;
+        pl.hist_multi.push_back(k);
+      }
+      if ((int)a < pl.nhist_big) pl.nhm_big = (int)pl.hist_multi.size();
+      a = b;
+    }
+  }
   long long small_max = 0;
   for (int i : pl.small) small_max = std::max(small_max, (long long)pl.desc[i].I * pl.desc[i].ld);
   pl.small_groups = small_admm_groups(small_max);
@@ -438,6 +472,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
+  pl.d_hist_multi = cv.take<Chunk>(pl.hist_multi.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
   pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
   pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
@@ -466,6 +501,7 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_hist_multi, pl.hist_multi.data(), pl.hist_multi.size() * sizeof(Chunk), s))) return rc;
   if (!pl.thin.empty() && (rc = h2d(pl.d_thin, pl.thin.data(), pl.thin.size() * sizeof(ThinUnit), s))) return rc;
   if (!pl.small.empty() && (rc = h2d(pl.d_small, pl.small.data(), pl.small.size() * sizeof(int), s))) return rc;
   return check_hip("upload");
@@ -608,6 +644,13 @@ int32_t admmq_get_solve_mode(void) { return g_solve_mode.load(); }
 
 // diagnostics (not in include/admmq.h): 1 (default) = finalize fused into the search
 // launch where its blocks are all resident, 0 = the separate finalize launch
+// diagnostics: stage-1 units per block of the non-fused search launch (0 = planner's choice)
+int32_t admmq_debug_set_search_units_per_block(int32_t reps) {
+  if (reps < 0 || reps > 64) return fail(ADMMQ_ERR_ARG, "units per block out of range");
+  g_hist_reps = reps;
+  return ADMMQ_OK;
+}
+
 int32_t admmq_debug_set_fused_finalize(int32_t enable) {
   g_fused_finalize = enable != 0;
   return ADMMQ_OK;
@@ -742,11 +785,13 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
     if (qscheme == kMse) {
       // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
-        const int nh = fuse_small ? pl.nhist_big : nhist;
+        // fused finalize: one whole-row unit per block; otherwise several units per block
+        const int nh = fuse_fin ? (fuse_small ? pl.nhist_big : nhist)
+                                : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
         if (nh > 0) {
           prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
-          launch_mse_hist3(pl.d_desc, nullptr, pl.d_hist, nh, num_attempts, bits, slot, pl.d_rank0, pl.d_groups,
-                           ngroups, pl.hist_nv, fuse_fin, it, s);
+          launch_mse_hist3(pl.d_desc, nullptr, fuse_fin ? pl.d_hist : pl.d_hist_multi, nh, num_attempts, bits, slot,
+                           pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, s);
           prof_mark(s);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each

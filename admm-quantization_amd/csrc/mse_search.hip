@@ -1041,17 +1041,32 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
   double s2 = 0.0;
+  // without the fused finalize a block may take several consecutive units of its job
+  // (ck.reps, `step` elements each): one table setup and one flush for all of them
+  const int reps = FIN ? 1 : max(ck.reps, 1);
+  for (int r = 0; r < reps; ++r) {
+    const long long ub = (long long)ck.start + (long long)r * ck.step;   // unit r (r > 0: reps > 1 only)
+    const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
+    if (r > 0) {   // this unit's elements (unit 0's were issued before the table setup)
 #pragma unroll
-  for (int hb = 0; hb < 2 * NV; hb += 2) {   // X - U (ADMM: H_T - U); zero past the end
-    float4 xa = x4[hb], xb = x4[hb + 1];
-    if (ck.U) { xa = sub4(xa, u4[hb]); xb = sub4(xb, u4[hb + 1]); }
-    const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hb;
-    if (e >= total) xa = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e + 2048 >= total) xb = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+      for (int hh = 0; hh < 2 * NV; ++hh) {
+        const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
+        x4[hh] = gld4(ck.X + (e < ue ? e : 0));
+        if (ck.U) u4[hh] = gld4(ck.U + (e < ue ? e : 0));
+      }
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
-    h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
+    for (int hb = 0; hb < 2 * NV; hb += 2) {   // X - U (ADMM: H_T - U); zero past the end
+      float4 xa = x4[hb], xb = x4[hb + 1];
+      if (ck.U) { xa = sub4(xa, u4[hb]); xb = sub4(xb, u4[hb + 1]); }
+      const long long e = ub + 4LL * threadIdx.x + 2048LL * hb;
+      if (e >= ue) xa = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e + 2048 >= ue) xb = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
+      h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
+    }
   }
   __syncthreads();
   const unsigned long long T2 = ADMMQ_NOW();
@@ -1080,7 +1095,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   __syncthreads();
   if (threadIdx.x == 0)
     last = (__hip_atomic_fetch_add(&v.ticket[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            (unsigned)(v.nhist - 1)) ? 1 : 0;
+            (unsigned)((ck.nblk > 0 ? ck.nblk : v.nhist) - 1)) ? 1 : 0;
   __syncthreads();
   const unsigned long long T3 = ADMMQ_NOW();
   auto trace = [&](unsigned long long T4) {

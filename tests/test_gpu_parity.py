@@ -393,16 +393,19 @@ def test_fused_finalize_equals_separate(torch_dev, eps):
                                                  ("layer3.1.conv2", 1), ("layer4.1.conv2", 0),
                                                  ("layer4.0.conv1", 1), ("layer1.1.conv2", 2)]]
 
-    def run(fused):
+    def run(fused, units=0):
         ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
               for H, F, G in probs_np]
-        with _lib.fused_finalize(fused):
+        with _lib.fused_finalize(fused), _lib.search_units_per_block(units):
             Hs, info = admm_iteration_batched(ps, 12, eps, 4, MSE, return_info=True)
         return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
 
     a, ia = run(True)
-    b, ib = run(False)
-    assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
-    assert np.array_equal(ia, ib)
-    for (ha, ua), (hb, ub) in zip(a, b):
-        assert _bits_equal(ha, hb) and _bits_equal(ua, ub)
+    # separate finalize launch; its search blocks take 1, 3 or 8 consecutive stage-1 units
+    # (one table setup and flush per block, ragged last group per job)
+    for units in (1, 3, 8):
+        b, ib = run(False, units)
+        assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
+        assert np.array_equal(ia, ib)
+        for (ha, ua), (hb, ub) in zip(a, b):
+            assert _bits_equal(ha, hb) and _bits_equal(ua, ub)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 session F (part 1, final tree): full GPU suite, then the rocprofv3 kernel-trace + PMC
+# Round-2 session F/I (part 1, final tree): full GPU suite, then the rocprofv3 kernel-trace + PMC
 # profiles of C3 / C4 / C5 (tools/profile.sh). Part 2 (tools/gpu_r02e.sh) runs the bench
 # lines once the traffic files are regenerated from these profiles.
 cd "$(dirname "$0")/.." || exit 1

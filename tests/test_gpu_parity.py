@@ -287,9 +287,17 @@ def test_iteration_count_and_early_exit(torch_dev, layer, mode):
     _, info = admm_iteration_batched([mk()], 7, 0.0, 4, MSE, return_info=True)
     assert info[0, 0].item() == 6 and info[0, 1].item() == 0
     p = mk()
-    (H,), info = admm_iteration_batched([p], 7, 1e30, 4, MSE, return_info=True)   # stops after the 1st iteration
+    (H,), dbg, info = admm_iteration_batched([p], 7, 1e30, 4, MSE, debug_outputs=True,
+                                             return_info=True)   # stops after the 1st iteration
     assert info[0, 0].item() == 1 and info[0, 1].item() == 1
-    Ho, Uo = ao.admm_iteration(H0, np.zeros_like(H0), F, G, 7, 1e30, 4, MSE)
+    Ho, Uo, oinfo = ao.admm_iteration(H0, np.zeros_like(H0), F, G, 7, 1e30, 4, MSE, return_info=True)
+    assert oinfo["iters"] == 1   # the oracle (source/admm.py:62-65) stops at the same iteration
+    HT, X = (t.cpu().numpy() for t in dbg[0])
+    assert np.linalg.norm(HT - oinfo["HT"]) / np.linalg.norm(oinfo["HT"]) < 1e-5
+    # the projection and the dual update of the stopped iteration, bit-exact given H_T
+    Hq = qo.quantize_tensor(X, 4, MSE)
+    assert _bits_equal(H.cpu().numpy(), Hq)
+    assert _bits_equal(p[1].cpu().numpy(), (np.zeros_like(H0) + (Hq - HT).astype(np.float32)).astype(np.float32))
     (H1,) = admm_iteration_batched([mk()], 2, 1e-8, 4, MSE)
     assert _bits_equal(H.cpu().numpy(), H1.cpu().numpy())
 

@@ -222,7 +222,7 @@ void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand
 
 constexpr int kSseQuads = 512;      // quads per stage-2 / exhaustive SSE work unit (8 KiB LDS)
 constexpr int kHistElems = 4096;    // elements per stage-1 work unit x hist_nv (1024 x 4 legacy, 512 x 8 merged)
-constexpr int kHistMultiRounds = 3;   // non-fused search: units per block sized for ~3 rounds of kHistMaxUnits blocks
+constexpr int kHistMultiRounds = 2;   // non-fused search: units per block sized for ~2 rounds of kHistMaxUnits blocks
 constexpr int kHistMultiMaxReps = 8;  // ... at most 8 units per block
 constexpr int kHistMaxUnits = 512;  // stage-1 units that fit in one round (2 per CU): above, 2x larger units
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)

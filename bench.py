@@ -343,6 +343,8 @@ def main():
                     help="per-iteration solve GEMM form: split-fp16 planes on f16 MFMA (default) or fp32 MFMA")
     ap.add_argument("--exhaustive", action="store_true",
                     help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
+    ap.add_argument("--search-units", type=int, default=0,
+                    help="A/B: stage-1 units per block of the non-fused search launch (0: the planner's choice)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -357,6 +359,7 @@ def main():
     lib = _lib.load()
     lib.admmq_set_exhaustive_search(1 if a.exhaustive else 0)
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
+    _lib.check(lib.admmq_debug_set_search_units_per_block(a.search_units), "search_units_per_block")
     split = a.solve == "split"
     work, numel, shard_info = build_workload(a.model, rank, world, a.shard, device)
     fi_per_step = sum(len(s.shape) * (a.max_iter_admm - 1) for (s, _, _, _) in work)

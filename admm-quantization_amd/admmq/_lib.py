@@ -23,12 +23,27 @@ SCHEMES = {
     "tensor_symmetric": 2,
     "tensor_affine": 3,
 }
+CHANNEL_SCHEMES = {"channel_symmetric": 4, "channel_affine": 5}
 
 
 class AdmmProblem(ctypes.Structure):
     _fields_ = [("F", ctypes.c_void_p), ("G", ctypes.c_void_p), ("H0", ctypes.c_void_p),
                 ("H_out", ctypes.c_void_p), ("U", ctypes.c_void_p), ("HT_out", ctypes.c_void_p),
                 ("X_out", ctypes.c_void_p), ("I", ctypes.c_int32), ("R", ctypes.c_int32)]
+
+
+class AdmmOptions(ctypes.Structure):
+    """admmq_admm_options (include/admmq.h): per-call solve form and fused finalize."""
+    _fields_ = [("solve_mode", ctypes.c_int32), ("fused_finalize", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+
+
+SOLVE_MODES = {"fp32": 0, "split": 1}
+
+
+def default_options() -> AdmmOptions:
+    o = AdmmOptions()
+    check(load().admmq_admm_default_options(ctypes.byref(o)), "default_options")
+    return o
 
 
 class QTensor(ctypes.Structure):
@@ -84,9 +99,16 @@ def load() -> ctypes.CDLL:
         "admmq_admm_prepare": (I32, [P, I32, I32, P, S, P]),
         "admmq_admm_run": (I32, [P, I32, I32, F32, I32, I32, I32, P, S, P, P]),
         "admmq_admm_iteration_batched": (I32, [P, I32, I32, F32, I32, I32, I32, P, S, P, P]),
+        "admmq_admm_default_options": (I32, [P]),
+        "admmq_admm_workspace_size_ex": (S, [P, I32, I32, P]),
+        "admmq_admm_prepare_ex": (I32, [P, I32, I32, P, P, S, P]),
+        "admmq_admm_run_ex": (I32, [P, I32, I32, F32, I32, I32, I32, P, P, S, P, P]),
+        "admmq_debug_set_fin_wait_polls": (I32, [ctypes.c_uint32]),
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
+        "admmq_quantize_channel_workspace_size": (S, [P, I32, I32]),
+        "admmq_quantize_channel": (I32, [P, P, P, I32, I32, I32, I32, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
         "admmq_set_solve_mode": (I32, [I32]),
         "admmq_get_solve_mode": (I32, []),
@@ -174,11 +196,11 @@ class exhaustive_search:
 
 
 class solve_mode:
-    """Context manager: the per-iteration solve's operand form, ``"split"`` (default:
-    fp16 hi/lo planes on f16 MFMA) or ``"fp32"`` (fp32 MFMA). Restores the previous
-    mode on exit."""
+    """Context manager: the process default of the per-iteration solve's operand form,
+    ``"fp32"`` (default: fp32 MFMA, the reference's arithmetic) or ``"split"`` (fp16
+    hi/lo planes on f16 MFMA, opt-in). Restores the previous mode on exit."""
 
-    MODES = {"fp32": 0, "split": 1}
+    MODES = SOLVE_MODES
 
     def __init__(self, mode: str):
         if mode not in self.MODES:
@@ -209,6 +231,22 @@ class fused_finalize:
 
     def __exit__(self, *exc):
         load().admmq_debug_set_fused_finalize(1)
+        return False
+
+
+class fin_wait_polls:
+    """Context manager (diagnostics): polls of the fused finalize's bounded wait for its
+    job's selection (1 forces the timeout / internal-fault path). Restores the default."""
+
+    def __init__(self, polls: int):
+        self.polls = polls
+
+    def __enter__(self):
+        check(load().admmq_debug_set_fin_wait_polls(int(self.polls)), "fin_wait_polls")
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_fin_wait_polls(0)
         return False
 
 

@@ -15,7 +15,7 @@ conventions:
 What differs by design: the Cholesky factor + per-iteration
 ``cholesky_solve`` are replaced by one fp64 blocked inverse per call and one
 fp32-MFMA GEMM per iteration, and the whole loop is a device-side launch
-sequence with no host synchronisation.
+sequence; the call synchronises once at its end (to check the fault column).
 
 ``admm_iteration_batched`` runs many independent (layer, mode) problems in the
 same launches; it is what the ALS driver and the benchmark use.
@@ -86,15 +86,21 @@ def _problem(H, U, F, G, HT_out=None, X_out=None):
 
 def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]],
                            max_iter: int, eps: float, bits: int, qscheme: str, num_attempts: int = 200,
-                           check_spd: bool = True, debug_outputs: bool = False, return_info: bool = False):
+                           check_spd: bool = True, debug_outputs: bool = False, return_info: bool = False,
+                           solve: Optional[str] = None):
     """Run ``admm_iteration`` on every (H, U, F, G) of ``problems`` in shared launches.
 
     Returns the list of new H tensors (and the caller's U tensors are updated in
     place). With ``return_info`` also returns an int32 tensor [n, 4] of
-    {iterations run, converged, spd_error, 0}; with ``debug_outputs`` a list of
-    (H_T, X) of the last iteration per problem. Calls ``torch.ops.admmq.admm_iteration_batched``
-    (csrc/torch_ops.cpp), which calls ``admmq_admm_prepare`` / ``admmq_admm_run``.
+    {iterations run, converged, spd_error, internal fault}; with ``debug_outputs`` a list
+    of (H_T, X) of the last iteration per problem. ``solve``: ``"fp32"`` (the process
+    default unless ``_lib.solve_mode`` changed it: fp32 MFMA, the reference's arithmetic)
+    or ``"split"`` for this call. Calls ``torch.ops.admmq.admm_iteration_batched``
+    (csrc/torch_ops.cpp), which calls ``admmq_admm_prepare_ex`` / ``admmq_admm_run_ex``;
+    an internal fault of the fused finalize (its bounded wait timed out) is repaired
+    inside the call by a re-run with the separate finalize launch.
     """
+    solve_code = -1 if solve is None else _lib.SOLVE_MODES[solve]
     if len(problems) == 0:
         return []
     for (H, U, F, G) in problems:
@@ -104,10 +110,11 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     code = _scheme_code(qscheme)
     if not _lib.use_ops():
         return _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd,
-                                            debug_outputs, return_info)
+                                            debug_outputs, return_info, solve_code)
     Hs, Us, Fs, Gs = (list(x) for x in zip(*problems))
     outs, info, hts, xs = _lib.ops().admm_iteration_batched(Hs, Us, Fs, Gs, int(max_iter), float(eps), int(bits), code,
-                                                            int(num_attempts), bool(check_spd), bool(debug_outputs))
+                                                            int(num_attempts), bool(check_spd), bool(debug_outputs),
+                                                            solve_code)
     ret = [list(outs) if max_iter > 1 else [p[0] for p in problems]]   # max_iter <= 1: the input H objects
     if debug_outputs:
         ret.append(list(zip(hts, xs)))
@@ -117,8 +124,10 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
 
 
 def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd, debug_outputs,
-                                 return_info):
-    """The same call through the C-ABI with ctypes (diagnostic builds, cross-checks)."""
+                                 return_info, solve_code=-1):
+    """The same call through the C-ABI with ctypes (diagnostic builds, cross-checks),
+    including the op's internal-fault repair (restore U, re-run without the fused finalize)."""
+    import ctypes
     lib = _lib.load()
     dev = problems[0][0].device
     Hs = [p[0].contiguous() for p in problems]
@@ -129,18 +138,22 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
     dbg = [(torch.empty_like(h), torch.empty_like(h)) for h in Hs] if debug_outputs else [(None, None)] * len(Hs)
     items = [_problem(H, U, F, G, *d) for H, U, F, G, d in zip(Hs, Us, Fs, Gs, dbg)]
     n = len(items)
+    opt = _lib.default_options()
+    if solve_code >= 0:
+        opt.solve_mode = solve_code
+    po = ctypes.byref(opt)
     arr = _lib.problems_array(items)
-    nb = lib.admmq_admm_workspace_size(arr, n, int(num_attempts))
+    nb = lib.admmq_admm_workspace_size_ex(arr, n, int(num_attempts), po)
     if nb == 0:
         _lib.check(-1, "admm workspace planning")
     ws = _lib.workspace(nb, dev)
     stream = _lib.stream_handle(dev)
-    _lib.check(lib.admmq_admm_prepare(arr, n, int(num_attempts), _lib.ptr(ws), nb, stream), "admm_prepare")
+    _lib.check(lib.admmq_admm_prepare_ex(arr, n, int(num_attempts), po, _lib.ptr(ws), nb, stream), "admm_prepare")
     info = torch.zeros(n * 4, dtype=torch.int32, device=dev)
     if check_spd or max_iter <= 1:
         # source/admm.py:54 raises before anything is modified: sync once per call
-        _lib.check(lib.admmq_admm_run(arr, n, 1, 0.0, 4, 0, int(num_attempts), _lib.ptr(ws), nb, _lib.ptr(info),
-                                      stream), "admm_info")
+        _lib.check(lib.admmq_admm_run_ex(arr, n, 1, 0.0, 4, 0, int(num_attempts), po, _lib.ptr(ws), nb, _lib.ptr(info),
+                                         stream), "admm_info")
         if int(info.view(n, 4)[:, 2].max().item()) != 0:
             raise torch.linalg.LinAlgError("linalg.cholesky: The factorization could not be completed because "
                                            "the input is not positive-definite.")
@@ -151,8 +164,21 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
     for it, o in zip(items, outs):
         it.H_out = o.data_ptr()
     arr = _lib.problems_array(items)
-    _lib.check(lib.admmq_admm_run(arr, n, int(max_iter), float(eps), int(bits), code, int(num_attempts),
-                                  _lib.ptr(ws), nb, _lib.ptr(info), stream), "admm_run")
+    ubak = [u.clone() for u in Us]
+
+    def run():
+        _lib.check(lib.admmq_admm_run_ex(arr, n, int(max_iter), float(eps), int(bits), code, int(num_attempts), po,
+                                         _lib.ptr(ws), nb, _lib.ptr(info), stream), "admm_run")
+
+    run()
+    if int(info.view(n, 4)[:, 3].max().item()) != 0:   # internal fault: repeat without the fused finalize
+        for u, b in zip(Us, ubak):
+            u.copy_(b)
+        opt.fused_finalize = 0
+        _lib.check(lib.admmq_admm_prepare_ex(arr, n, int(num_attempts), po, _lib.ptr(ws), nb, stream), "admm_prepare")
+        run()
+        if int(info.view(n, 4)[:, 3].max().item()) != 0:
+            raise RuntimeError("admmq: internal fault in the separate-finalize re-run")
     for u_user, u in zip(Us_user, Us):
         if u is not u_user:
             u_user.copy_(u)
@@ -165,7 +191,7 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
 
 
 def admm_iteration(H: torch.Tensor, U: torch.Tensor, F: torch.Tensor, G: torch.Tensor, max_iter: int, eps: float,
-                   bits: int, qscheme: str, num_attempts: int = 200):
+                   bits: int, qscheme: str, num_attempts: int = 200, solve: Optional[str] = None):
     """source/admm.py:51-67 -> (H_new, U)."""
-    out = admm_iteration_batched([(H, U, F, G)], max_iter, eps, bits, qscheme, num_attempts=num_attempts)
+    out = admm_iteration_batched([(H, U, F, G)], max_iter, eps, bits, qscheme, num_attempts=num_attempts, solve=solve)
     return out[0], U

@@ -77,10 +77,15 @@ class LayerRun:
 
 
 def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: int, qscheme: str,
-              num_attempts: int = 200, record_errors: bool = True, tol: float = 1e-5):
+              num_attempts: int = 200, record_errors: bool = True, tol: float = 1e-5, solve: Optional[str] = None):
     """One ALS sweep over all active layers (modes batched across layers). Returns the
     factor-iterations the inner ADMM loops ran in this sweep, per active layer
-    (``{id(run): count}``)."""
+    (``{id(run): count}``).
+
+    SPD failures are read once per sweep (one host sync): a ``LinAlgError`` is raised
+    after every mode of the sweep has run, so - unlike the reference, which raises at
+    the Cholesky call before changing anything (``source/admm.py:54``) - the runs'
+    factors, duals and quantized factors are undefined after the error."""
     act = [r for r in runs if r.active]
     nmodes = max((len(r.factors) for r in act), default=0)
     infos = []
@@ -90,7 +95,7 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
         probs = [(r.factors[mode], r.duals[mode], F, G) for r, (G, F) in zip(sel, GF)]
         # no per-call sync for the SPD test: the flags are read once per sweep (below)
         Hs, info = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
-                                          check_spd=False, return_info=True)
+                                          check_spd=False, return_info=True, solve=solve)
         infos.append(info[:, [0, 2]])   # {iterations run, spd_error}
         for r, H in zip(sel, Hs):
             r.factors[mode] = H

@@ -7,7 +7,10 @@ reference's names, argument meaning and error behaviour:
   (``quantize_tensor_mse``, :118-144; ``num_attempts`` via kwargs);
 * ``tensor_minmax`` -> ``min_max_quantize`` (:48-66);
 * ``tensor_symmetric`` / ``tensor_affine`` -> :91-106 (``tmin``/``tmax`` kwargs);
-* ``channel_*`` with ``dim=None`` raise ``TypeError`` (the reference fails in
+* ``channel_symmetric`` / ``channel_affine`` with an explicit ``dim`` -> per-channel
+  statistics of ``unfold(tensor, dim)`` broadcast against the tensor's last dimension,
+  exactly as the reference's torch code does (:29-33, 91-106; an incompatible size raises
+  the same ``RuntimeError``); ``dim=None`` raises ``TypeError`` (the reference fails in
   ``unfold(tensor, None)``); ``tensor_log`` and unknown names raise
   ``NotImplementedError``.
 
@@ -24,16 +27,16 @@ import torch
 
 from . import _lib
 
-__all__ = ["quantize_tensor", "quantize_tensor_mse", "min_max_quantize", "quantize_batched", "get_tensor_stats",
+__all__ = ["quantize_tensor", "quantize_channel", "quantize_tensor_mse", "min_max_quantize", "quantize_batched", "get_tensor_stats",
            "mse_sse_table"]
 
 
 def _scheme_code(qscheme: str, dim=None) -> int:
-    if qscheme in ("channel_symmetric", "channel_affine"):
+    if qscheme in _lib.CHANNEL_SCHEMES:
         if dim is None:
             raise TypeError("Can't collect per-channel statistics with dim=None "
                             "(reference: unfold(tensor, mode=None))")
-        raise NotImplementedError(f"{qscheme}: per-channel quantization is outside the ADMM hot path")
+        return _lib.CHANNEL_SCHEMES[qscheme]
     if qscheme not in _lib.SCHEMES:
         raise NotImplementedError(qscheme)
     return _lib.SCHEMES[qscheme]
@@ -82,9 +85,46 @@ def quantize_batched(tensors: Sequence[torch.Tensor], bits: int, qscheme: str, n
     return outs
 
 
+def quantize_channel(tensor: torch.Tensor, bits: int, qscheme: str, dim: int) -> torch.Tensor:
+    """``channel_symmetric`` / ``channel_affine`` with an explicit ``dim``
+    (``source/quantization.py:29-33, 91-106``) on the device (``admmq_quantize_channel``)."""
+    code = _scheme_code(qscheme, dim)
+    _lib.require_device(tensor)
+    if bits < 1:
+        raise AssertionError(bits)
+    if tensor.dim() == 0:
+        raise IndexError(f"Dimension out of range (expected to be in range of [-1, 0], but got {dim})")
+    x = tensor.contiguous()
+    if _lib.use_ops():
+        return _lib.ops().quantize_channel(x, int(bits), code, int(dim))
+    import ctypes
+    lib = _lib.load()
+    nd = x.dim()
+    d = dim + nd if dim < 0 else dim
+    if not 0 <= d < nd:
+        raise IndexError(f"Dimension out of range (expected to be in range of [{-nd}, {nd - 1}], but got {dim})")
+    C, L = x.shape[d], x.shape[-1]
+    if L != C and L != 1 and C != 1:
+        raise RuntimeError(f"The size of tensor a ({L}) must match the size of tensor b ({C}) at non-singleton "
+                           f"dimension {nd - 1}")
+    shape = (ctypes.c_int64 * nd)(*x.shape)
+    y = torch.empty(tuple(x.shape[:-1]) + (max(L, C),), dtype=x.dtype, device=x.device)
+    nb = lib.admmq_quantize_channel_workspace_size(shape, nd, d)
+    ws = _lib.workspace(nb, x.device)
+    _lib.check(lib.admmq_quantize_channel(_lib.ptr(x), _lib.ptr(y), shape, nd, d, int(bits), code, _lib.ptr(ws), nb,
+                                          _lib.stream_handle(x.device)), "quantize_channel")
+    return y
+
+
 def quantize_tensor(tensor: torch.Tensor, bits: int, qscheme: str, dim=None, **kwargs) -> torch.Tensor:
     """source/quantization.py:69-115."""
     code = _scheme_code(qscheme, dim)
+    if code in (4, 5):
+        if code == 5 and kwargs.get("tmin") is not None and kwargs.get("tmax") is not None:
+            # explicit range: the statistics are not collected, so the channel scheme is the
+            # tensor scheme with that range (source/quantization.py:98-101)
+            return quantize_tensor(tensor, bits, "tensor_affine", tmin=kwargs["tmin"], tmax=kwargs["tmax"])
+        return quantize_channel(tensor, bits, qscheme, dim)
     num_attempts = int(kwargs.get("num_attempts", 200)) if code == 0 else 200
     tmin = kwargs.get("tmin") if code == 3 else None
     tmax = kwargs.get("tmax") if code == 3 else None

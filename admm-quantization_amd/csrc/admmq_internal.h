@@ -203,7 +203,10 @@ int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out)
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      hipStream_t s);
+                      unsigned wait_polls, hipStream_t s);
+// fused finalize: polls (s_sleep 2 each, ~10 ms in all) before a block gives up waiting for
+// its job's selection and reports an internal fault instead of finalizing
+constexpr unsigned kFinWaitPollsDefault = 1u << 17;
 int hist3_fin_capacity(int ncand, int bits, int nv);
 int small_admm_groups(long long maxtotal);
 void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ngr, int ncand, int bits, int slot,
@@ -217,6 +220,8 @@ void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, i
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
 
 void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s);
+void launch_channel_quant(const float* x, float* y, long long A, int C, long long B, long long outer, int L, int Lo,
+                          unsigned* stats, int bits, int scheme, hipStream_t s);
 void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
                    hipStream_t s);
 

@@ -9,6 +9,8 @@
 #include <string>
 #include <array>
 #include <map>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/admmq.h"
@@ -61,15 +63,33 @@ static Prof g_prof;
 // Process-wide switches (atomics: set from any thread, read by the launch sequences).
 // exhaustive: evaluate all candidates (reference-style) instead of the two-stage search;
 // legacy stage 1: the per-level stage-1 form instead of merged thresholds (same integers);
-// solve mode: kSolveSplit (default) or kSolveF32 for the per-iteration GEMM.
+// solve mode: the process default (kSolveF32: the reference's fp32 arithmetic; kSolveSplit
+// opt-in) of the plain entry points, read once at prepare and recorded per workspace.
 static std::atomic<bool> g_exhaustive{false};
 static std::atomic<bool> g_legacy_stage1{false};
-static std::atomic<int> g_solve_mode{kSolveSplit};
+static std::atomic<int> g_solve_mode{kSolveF32};
 // fused finalize (k_mse_hist3<.., true>) where the residency check allows it; 0: the
 // separate k_finalize_admm launch (A/B and cross-check, same integers)
 static std::atomic<bool> g_fused_finalize{true};
 // stage-1 units per block of the non-fused search launch (0: sized by the planner)
 static std::atomic<int> g_hist_reps{0};
+// polls of the fused finalize's bounded wait for its job's selection (diagnostics can
+// shrink it to force the timeout path)
+static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
+
+// Solve mode recorded by each prepare for its workspace (the run must use the operand
+// planes its prepare wrote: the per-problem buffer carve depends on the mode).
+static std::mutex g_ws_mu;
+static std::unordered_map<const void*, int> g_ws_mode;
+static void record_ws_mode(const void* ws, int mode) {
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  g_ws_mode[ws] = mode;
+}
+static int recorded_ws_mode(const void* ws) {
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  auto it = g_ws_mode.find(ws);
+  return it == g_ws_mode.end() ? -1 : it->second;
+}
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
 static bool two_stage_ok(int ncand, int bits) {
@@ -246,7 +266,7 @@ static int fin_groups_for(const std::vector<ProbDesc>& desc, const std::vector<i
   return g;
 }
 
-static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl) {
+static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl, int solve_mode) {
   if (nprob <= 0 || !probs) return fail(ADMMQ_ERR_ARG, "no problems");
   if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
   Carver cv(ws);
@@ -254,7 +274,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.thin_nr = 0;
   for (int i = 0; i < nprob; ++i)
     if (probs[i].I > 0 && probs[i].I <= kThinRows) pl.thin_nr = std::max(pl.thin_nr, probs[i].I);
-  pl.split = g_solve_mode.load() == kSolveSplit;
+  pl.split = solve_mode == kSolveSplit;
   // Wide tiles when the 64x64 tiles would take many rounds of the resident slots
   // (256 CUs x 3): then a CU's bytes per MAC matter more than the number of tiles, and
   // 256x128 tiles read 3/8 of the operand bytes per MAC (the Llama shapes of C5). The
@@ -606,7 +626,7 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
       if ((rc = h2d(pl.d_rank0, rank0.data(), rank0.size() * 2, s))) return rc;
       if (!groups.empty() && (rc = h2d(pl.d_groups, groups.data(), groups.size() * 2, s))) return rc;
       launch_mse_hist3(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, pl.d_rank0,
-                       pl.d_groups, (int)groups.size() / 6, 1, false, 0, s);
+                       pl.d_groups, (int)groups.size() / 6, 1, false, 0, 0u, s);
     } else if (!all) {
       launch_mse_hist(nullptr, pl.d_jobs, pl.d_hist, (int)pl.hist_chunks.size(), ncand, bits, 0, 1, s);
     } else {   // exhaustive: every candidate's canonical SSE over all chunks
@@ -661,8 +681,15 @@ int32_t admmq_debug_set_fused_finalize(int32_t enable) {
 // and the real carve agree
 size_t admmq_debug_admm_plan_bytes(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* base) {
   AdmmPlan pl;
-  if (plan_admm(probs, nprob, num_attempts, base, pl) != ADMMQ_OK) return 0;
+  if (plan_admm(probs, nprob, num_attempts, base, pl, g_solve_mode.load()) != ADMMQ_OK) return 0;
   return pl.bytes;
+}
+
+// diagnostics (not in include/admmq.h): polls of the fused finalize's bounded wait
+// (default kFinWaitPollsDefault; a test sets 1 to force the timeout / internal-fault path)
+int32_t admmq_debug_set_fin_wait_polls(uint32_t polls) {
+  g_fin_wait_polls = polls ? polls : kFinWaitPollsDefault;
+  return ADMMQ_OK;
 }
 
 // diagnostics (not in include/admmq.h): 1 = per-level stage 1, 0 = merged thresholds
@@ -707,16 +734,48 @@ int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class) {
 
 const char* admmq_last_error(void) { return g_err.c_str(); }
 
-size_t admmq_admm_workspace_size(const admmq_problem* probs, int32_t nprob, int32_t num_attempts) {
+static int check_opts(const admmq_admm_options* o) {
+  if (!o) return fail(ADMMQ_ERR_ARG, "options must not be NULL");
+  if (o->solve_mode != kSolveF32 && o->solve_mode != kSolveSplit)
+    return fail(ADMMQ_ERR_ARG, "solve_mode must be ADMMQ_SOLVE_FP32 or ADMMQ_SOLVE_SPLIT");
+  if (o->fused_finalize != 0 && o->fused_finalize != 1) return fail(ADMMQ_ERR_ARG, "fused_finalize must be 0 or 1");
+  for (int r : o->reserved)
+    if (r != 0) return fail(ADMMQ_ERR_ARG, "reserved option fields must be zero");
+  return ADMMQ_OK;
+}
+static admmq_admm_options default_opts() {
+  admmq_admm_options o;
+  std::memset(&o, 0, sizeof(o));
+  o.solve_mode = g_solve_mode.load();
+  o.fused_finalize = g_fused_finalize.load() ? 1 : 0;
+  return o;
+}
+
+int32_t admmq_admm_default_options(admmq_admm_options* out) {
+  if (!out) return fail(ADMMQ_ERR_ARG, "options must not be NULL");
+  *out = default_opts();
+  return ADMMQ_OK;
+}
+
+size_t admmq_admm_workspace_size_ex(const admmq_problem* probs, int32_t nprob, int32_t num_attempts,
+                                    const admmq_admm_options* opt) {
+  if (check_opts(opt)) return 0;
   AdmmPlan pl;
-  if (plan_admm(probs, nprob, num_attempts, nullptr, pl) != ADMMQ_OK) return 0;
+  if (plan_admm(probs, nprob, num_attempts, nullptr, pl, opt->solve_mode) != ADMMQ_OK) return 0;
   return pl.bytes;
 }
 
-int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* workspace,
-                           size_t workspace_bytes, void* stream) {
+size_t admmq_admm_workspace_size(const admmq_problem* probs, int32_t nprob, int32_t num_attempts) {
+  const admmq_admm_options o = default_opts();
+  return admmq_admm_workspace_size_ex(probs, nprob, num_attempts, &o);
+}
+
+int32_t admmq_admm_prepare_ex(const admmq_problem* probs, int32_t nprob, int32_t num_attempts,
+                              const admmq_admm_options* opt, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_opts(opt);
+  if (rc) return rc;
   AdmmPlan pl;
-  int rc = plan_admm(probs, nprob, num_attempts, workspace, pl);
+  rc = plan_admm(probs, nprob, num_attempts, workspace, pl, opt->solve_mode);
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -731,16 +790,29 @@ int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t nu
     launch_split_rows(pl.d_desc, nprob, pl.maxIp, 0, s);
   }
   prof_mark(s);
-  return check_hip("admm_prepare");
+  if ((rc = check_hip("admm_prepare"))) return rc;
+  record_ws_mode(workspace, opt->solve_mode);
+  return ADMMQ_OK;
 }
 
-int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
-                       int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
-                       int32_t* info, void* stream) {
+int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t num_attempts, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  const admmq_admm_options o = default_opts();
+  return admmq_admm_prepare_ex(probs, nprob, num_attempts, &o, workspace, workspace_bytes, stream);
+}
+
+int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
+                          int32_t qscheme, int32_t num_attempts, const admmq_admm_options* opt, void* workspace,
+                          size_t workspace_bytes, int32_t* info, void* stream) {
+  int rc = check_opts(opt);
+  if (rc) return rc;
   if (!valid_scheme(qscheme)) return fail(ADMMQ_ERR_SCHEME, "unknown qscheme");
   if (!valid_bits(bits)) return fail(ADMMQ_ERR_ARG, "bits out of range");
+  const int rec = recorded_ws_mode(workspace);
+  if (rec < 0) return fail(ADMMQ_ERR_ARG, "admm_run: the workspace has not been prepared (admmq_admm_prepare)");
+  if (rec != opt->solve_mode) return fail(ADMMQ_ERR_ARG, "admm_run: solve_mode differs from the one its prepare used");
   AdmmPlan pl;
-  int rc = plan_admm(probs, nprob, num_attempts, workspace, pl);
+  rc = plan_admm(probs, nprob, num_attempts, workspace, pl, rec);
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -762,9 +834,11 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   const bool fuse_small = qscheme == kMse && !exhaustive && merged && !pl.small.empty() &&
                           pl.small_groups > 0 && num_attempts <= 1024;
   // the big jobs' finalize inside the search launch when all its blocks fit at once
+  // (with a margin of one resident block per CU: see hist3_fin_capacity)
   const int nh_big = fuse_small ? pl.nhist_big : nhist;
-  const bool fuse_fin = g_fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0 &&
-                        nh_big <= hist3_fin_capacity(num_attempts, bits, pl.hist_nv);
+  const bool fuse_fin = opt->fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned &&
+                        nh_big > 0 && nh_big <= hist3_fin_capacity(num_attempts, bits, pl.hist_nv);
+  const unsigned polls = g_fin_wait_polls.load();
   if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned), s) != hipSuccess)
     return check_hip("ready reset");
   for (int it = 0; it + 1 < max_iter; ++it) {
@@ -791,7 +865,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
         if (nh > 0) {
           prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
           launch_mse_hist3(pl.d_desc, nullptr, fuse_fin ? pl.d_hist : pl.d_hist_multi, nh, num_attempts, bits, slot,
-                           pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, s);
+                           pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s);
           prof_mark(s);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each
@@ -825,6 +899,16 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
   return check_hip("admm_run");
 }
 
+int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
+                       int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
+                       int32_t* info, void* stream) {
+  admmq_admm_options o = default_opts();
+  const int rec = recorded_ws_mode(workspace);   // the mode this workspace was prepared with
+  if (rec >= 0) o.solve_mode = rec;
+  return admmq_admm_run_ex(probs, nprob, max_iter, eps, bits, qscheme, num_attempts, &o, workspace, workspace_bytes,
+                           info, stream);
+}
+
 // diagnostics (not in include/admmq.h): per-block timelines of the last launches (make TRACE=1)
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
@@ -843,6 +927,53 @@ int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, 
   if (rc) return rc;
   return admmq_admm_run(probs, nprob, max_iter, eps, bits, qscheme, num_attempts, workspace, workspace_bytes, info,
                         stream);
+}
+
+// (A, C, B) around the channel dim and the broadcast output shape (outer x Lo); false:
+// invalid arguments (error recorded)
+static bool channel_geometry(const int64_t* shape, int32_t ndim, int32_t dim, long long& A, int& C, long long& B,
+                             long long& outer, int& L, int& Lo) {
+  if (!shape || ndim < 1 || ndim > 16) { fail(ADMMQ_ERR_ARG, "channel quantization needs 1 <= ndim <= 16"); return false; }
+  if (dim < -ndim || dim >= ndim) { fail(ADMMQ_ERR_ARG, "dim out of range"); return false; }
+  const int d = dim < 0 ? dim + ndim : dim;
+  A = 1; B = 1;
+  for (int k = 0; k < ndim; ++k) {
+    if (shape[k] <= 0) { fail(ADMMQ_ERR_ARG, "empty tensor"); return false; }
+    if (k < d) A *= shape[k];
+    if (k > d) B *= shape[k];
+  }
+  if (shape[d] > (1 << 30) || A * B * shape[d] > (1LL << 40)) { fail(ADMMQ_ERR_ARG, "tensor too large"); return false; }
+  C = (int)shape[d];
+  L = (int)shape[ndim - 1];
+  if (L != C && L != 1 && C != 1) {
+    fail(ADMMQ_ERR_ARG, "the channel statistics do not broadcast against the last dimension");
+    return false;
+  }
+  Lo = std::max(L, C);
+  outer = A * B * C / L;
+  return true;
+}
+
+size_t admmq_quantize_channel_workspace_size(const int64_t* shape, int32_t ndim, int32_t dim) {
+  long long A, B, outer;
+  int C, L, Lo;
+  if (!channel_geometry(shape, ndim, dim, A, C, B, outer, L, Lo)) return 0;
+  return align_up((size_t)3 * C * sizeof(unsigned), 256);
+}
+
+int32_t admmq_quantize_channel(const float* x, float* y, const int64_t* shape, int32_t ndim, int32_t dim, int32_t bits,
+                               int32_t qscheme, void* workspace, size_t workspace_bytes, void* stream) {
+  if (qscheme != ADMMQ_CHANNEL_SYMMETRIC && qscheme != ADMMQ_CHANNEL_AFFINE)
+    return fail(ADMMQ_ERR_SCHEME, "qscheme must be ADMMQ_CHANNEL_SYMMETRIC or ADMMQ_CHANNEL_AFFINE");
+  if (!valid_bits(bits) || bits > 31) return fail(ADMMQ_ERR_ARG, "bits out of range");
+  if (!x || !y) return fail(ADMMQ_ERR_ARG, "null tensor");
+  long long A, B, outer;
+  int C, L, Lo;
+  if (!channel_geometry(shape, ndim, dim, A, C, B, outer, L, Lo)) return ADMMQ_ERR_ARG;
+  if (!workspace || workspace_bytes < (size_t)3 * C * sizeof(unsigned)) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  launch_channel_quant(x, y, A, C, B, outer, L, Lo, static_cast<unsigned*>(workspace), bits,
+                       qscheme == ADMMQ_CHANNEL_SYMMETRIC ? kSymmetric : kAffine, static_cast<hipStream_t>(stream));
+  return check_hip("quantize_channel");
 }
 
 size_t admmq_quantize_workspace_size(const admmq_qtensor* t, int32_t n, int32_t num_attempts) {

@@ -15,6 +15,7 @@
 // stage 2  k_mse_sse    canonical SSE only for c in S (|S| = 1 almost always: then the
 //                       kernel exits at once); exhaustive when |S| > kMaxSel or forced.
 #include <algorithm>
+#include <mutex>
 #include <cstdlib>
 
 #include "quant_device.h"
@@ -960,17 +961,17 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
 // selection. The last block of a job publishes the selection record with write-through
 // (sc1) stores, then the job's ready word = iter + 1; the others poll that word (one
 // wave, relaxed agent-scope loads with s_sleep) and read the record with sc1 loads. The
-// wait is bounded: past ~10 ms the block stops waiting, sets flags[3] (reported as an
-// internal fault by admmq_admm_run's info) and finishes, so a broken residency
-// assumption cannot hang the GPU. Saves the finalize launch, its dependent parameter
-// chain and its re-read of H_T and U.
-constexpr unsigned kFinWaitPolls = 1u << 17;
-
+// wait is bounded (`wait_polls`, ~10 ms by default): past it the block sets flags[3]
+// (reported as an internal fault in admmq_admm_run's info) and ends WITHOUT finalizing
+// its elements, so a broken residency assumption can neither hang the GPU nor finalize
+// with a stale selection record; the caller re-runs the call with the separate finalize
+// launch (the PyTorch op does). Saves the finalize launch, its dependent parameter chain
+// and its re-read of H_T and U.
 template <int QMAX, int NV, bool FIN>
 __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     const ProbDesc* __restrict__ d, const QJob* __restrict__ qj, const Chunk* __restrict__ chunks, int ncand, int slot,
     const unsigned short* __restrict__ rank0, const unsigned short* __restrict__ groups, int ngroups, int bits,
-    int iter) {
+    int iter, unsigned wait_polls) {
   const unsigned long long T0 = ADMMQ_NOW();
   const Chunk ck = chunks[blockIdx.x];
   // first-needed inputs straight from the unit (one dependent level): stop flag, max|x|,
@@ -1003,6 +1004,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   __shared__ unsigned long long wtot[8], wtot2[8];
   __shared__ unsigned wtot32[8], wtot32b[8];
   __shared__ int last;
+  __shared__ int timed_out;
   __shared__ int lsel[2 + kMaxSel];
   const int n = ncand;
   // the finalize step's other inputs (current H, padded F): issued after the search
@@ -1165,17 +1167,24 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     if (!last) {   // wait for the job's selection (bounded)
       if (threadIdx.x == 0) {
         unsigned polls = 0;
+        int to = 0;
         while (__hip_atomic_load(v.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)(iter + 1)) {
           __builtin_amdgcn_s_sleep(2);
-          if (++polls == kFinWaitPolls) {
+          if (++polls >= wait_polls) {
             __hip_atomic_store(p.flags + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            to = 1;
             break;
           }
         }
+        timed_out = to;
         lsel[0] = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         lsel[2] = __hip_atomic_load(sel + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
+      if (timed_out) {   // internal fault: leave the elements unfinalized (the caller re-runs)
+        __builtin_amdgcn_s_waitcnt(0);
+        return;
+      }
     }
     QParams qp;
     if (lsel[0] == 1) {
@@ -1444,12 +1453,12 @@ bool merged_ok(int ncand, int bits) {
 }
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      hipStream_t s) {
+                      unsigned wait_polls, hipStream_t s) {
   if (nchunks <= 0) return;
   const size_t lds = hist3_lds_bytes(ncand, bits);
 #define ADMMQ_H3(Q, V, F)                                                                                        \
   hipLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, d, q, chunks, ncand, slot, \
-                     rank0, groups, ngroups, bits, iter)
+                     rank0, groups, ngroups, bits, iter, wait_polls)
 #define ADMMQ_H3N(Q)                               \
   if (fin) {                                       \
     if (nv == 2) ADMMQ_H3(Q, 2, true);             \
@@ -1469,16 +1478,24 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
 #undef ADMMQ_H3
 }
 
-// Resident blocks of the fused (FIN) search kernel on this device (all of a launch's
-// blocks must be resident at once for its in-kernel wait): occupancy x CUs.
+// Resident blocks of the fused (FIN) search kernel on the CURRENT device (all of a
+// launch's blocks must be resident at once for its in-kernel wait): occupancy x CUs.
+// The occupancy API cannot see other work on the device (a kernel of another stream,
+// RCCL): a wait that times out because of it is reported as an internal fault and its
+// elements are left unfinalized (k_mse_hist3), and the caller re-runs the call with the
+// separate finalize launch. (A one-block-per-CU margin would disable the fused form at
+// C3: 371 units against 2 x 256 resident blocks, 63 KB of LDS each.) The CU count is
+// looked up once per device.
 int hist3_fin_capacity(int ncand, int bits, int nv) {
-  static int cus = -1;
-  if (cus < 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess)
-      cus = 0;
-  }
+  constexpr int kMaxDev = 64;
+  static std::once_flag once[kMaxDev];
+  static int cus[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+  std::call_once(once[dev], [dev]() {
+    int n = 0;
+    cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
+  });
   const size_t lds = hist3_lds_bytes(ncand, bits);
   int per = 0;
   hipError_t e = hipErrorInvalidValue;
@@ -1493,7 +1510,7 @@ int hist3_fin_capacity(int ncand, int bits, int nv) {
     default: ADMMQ_OCC(16); break;
   }
 #undef ADMMQ_OCC
-  return e == hipSuccess ? per * cus : 0;
+  return e == hipSuccess ? per * cus[dev] : 0;
 }
 void launch_mse_select_all(const ProbDesc* d, const QJob* q, int njobs, int ncand, int slot, hipStream_t s) {
   if (njobs > 0) hipLaunchKernelGGL(k_mse_select_all, dim3(njobs), dim3(64), 0, s, d, q, ncand, slot);

@@ -64,6 +64,66 @@ __global__ __launch_bounds__(256) void k_qfinal(const QJob* __restrict__ jobs, c
   }
 }
 
+// Per-channel schemes (channel_symmetric / channel_affine with an explicit dim,
+// source/quantization.py:29-33, 91-106). The tensor is viewed as (A, C, B) around the
+// channel dimension dim (C = shape[dim]); channel r = row r of unfold(x, dim)
+// (source/utils.py:60-74). One block per channel: min / max as order-preserving
+// encodings, plus a NaN flag (torch's max / min propagate NaN).
+__global__ __launch_bounds__(256) void k_channel_stats(const float* __restrict__ x, long long A, int C, long long B,
+                                                       unsigned* __restrict__ stats) {
+  const int r = blockIdx.x;
+  const long long n = A * B;
+  unsigned mn = 0xFFFFFFFFu, mxo = 0u, nan = 0u;
+  for (long long t = threadIdx.x; t < n; t += blockDim.x) {
+    const long long a = t / B, b = t - a * B;
+    const float v = x[(a * C + r) * B + b];
+    if (v != v) {
+      nan = 1u;
+    } else {
+      const unsigned e = enc_ord(v);
+      mn = min(mn, e);
+      mxo = max(mxo, e);
+    }
+  }
+  __shared__ unsigned red[3][4];
+  mn = wave_min_u32(mn); mxo = wave_max_u32(mxo); nan = wave_max_u32(nan);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = mn; red[1][w] = mxo; red[2][w] = nan; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      mn = min(mn, red[0][k]); mxo = max(mxo, red[1][k]); nan = max(nan, red[2][k]);
+    }
+    stats[3 * r + 0] = mn;
+    stats[3 * r + 1] = mxo;
+    stats[3 * r + 2] = nan;
+  }
+}
+
+// y (outer x Lo) = the scheme applied to x (outer x L) with the statistics of channel
+// (C == 1 ? 0 : j) for output column j: torch broadcasts the (C,) statistics against the
+// tensor's last dimension (the host checked L == C or one of them is 1; Lo = max(L, C)).
+__global__ __launch_bounds__(256) void k_channel_quant(const float* __restrict__ x, float* __restrict__ y,
+                                                       long long nout, int L, int Lo, int C,
+                                                       const unsigned* __restrict__ stats, int bits, int scheme) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nout) return;
+  const long long o = i / Lo;
+  const int j = (int)(i - o * Lo);
+  const int ci = C == 1 ? 0 : j;
+  const float tmin = dec_ord(stats[3 * ci + 0]), tmax = dec_ord(stats[3 * ci + 1]);
+  const QParams qp = qparams_stats(scheme, bits, tmin, tmax, (int)stats[3 * ci + 2], 0, 0.f, 0.f);
+  y[i] = apply_quant(x[o * L + (L == 1 ? 0 : j)], qp);
+}
+
+void launch_channel_quant(const float* x, float* y, long long A, int C, long long B, long long outer, int L, int Lo,
+                          unsigned* stats, int bits, int scheme, hipStream_t s) {
+  hipLaunchKernelGGL(k_channel_stats, dim3(C), dim3(256), 0, s, x, A, C, B, stats);
+  const long long nout = outer * Lo;
+  hipLaunchKernelGGL(k_channel_quant, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, s, x, y, nout, L, Lo, C,
+                     stats, bits, scheme);
+}
+
 void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s) {
   if (nchunks > 0) hipLaunchKernelGGL(k_qpack, dim3(nchunks), dim3(256), 0, s, jobs, chunks);
 }

@@ -11,6 +11,8 @@
  *                                           (batched over independent (layer, mode) problems)
  *   admmq_quantize_batched               <- source/quantization.py:69-115  quantize_tensor(tensor,bits,qscheme,**kw)
  *                                           incl. quantize_tensor_mse :118-144, min_max_quantize :48-66
+ *   admmq_quantize_channel               <- source/quantization.py:69-106 quantize_tensor(tensor,bits,
+ *                                           'channel_symmetric' | 'channel_affine', dim)
  *   admmq_mse_sse_table                  <- source/quantization.py:129-141 (the candidate search, exposed
  *                                           for parity tests: canonical fixed-point SSE per candidate)
  *   admmq_cp_gram_mttkrp                 <- scripts/factorize.py:215-237 (3-way) and :276-287 (2-way):
@@ -69,10 +71,40 @@ int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t nu
 /* The loop of source/admm.py:55-65: max_iter-1 iterations of {solve, quantize,
  * dual update, residual test} per problem, with the per-problem early exit when
  * r < eps and s < eps. Writes H_out and U. info (device int32[nprob*4], may be
- * NULL) receives {iterations run, converged, spd_error, 0} per problem. */
+ * NULL) receives {iterations run, converged, spd_error, internal fault} per problem
+ * (internal fault: see admmq_admm_run_ex). Uses the solve mode its prepare recorded;
+ * ADMMQ_ERR_ARG for a workspace no prepare has set up. */
 int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
                        int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
                        int32_t* info, void* stream);
+
+/* Per-call options of the ADMM entry points (the _ex forms). A prepare fixes the
+ * operand form of the solve for its workspace: a run on that workspace must ask for the
+ * same solve_mode (ADMMQ_ERR_ARG otherwise). The plain forms above take the process
+ * defaults (admmq_set_solve_mode) at prepare; their run uses what its prepare recorded. */
+#define ADMMQ_SOLVE_FP32 0  /* v_mfma_f32_32x32x2_f32: an fp32 FMA chain, the reference's arithmetic (default) */
+#define ADMMQ_SOLVE_SPLIT 1 /* split fp16 planes on f16 MFMA (about 2^-21 relative per product; opt-in) */
+typedef struct admmq_admm_options {
+  int32_t solve_mode;     /* ADMMQ_SOLVE_FP32 or ADMMQ_SOLVE_SPLIT */
+  int32_t fused_finalize; /* 1: projection + dual update inside the search launch where all its blocks are
+                             resident at once; 0: always the separate finalize launch (same results) */
+  int32_t reserved[6];    /* must be zero */
+} admmq_admm_options;
+
+/* Fills *out with the process defaults (admmq_set_solve_mode; fused finalize on). */
+int32_t admmq_admm_default_options(admmq_admm_options* out);
+size_t admmq_admm_workspace_size_ex(const admmq_problem* probs, int32_t nprob, int32_t num_attempts,
+                                    const admmq_admm_options* opt);
+int32_t admmq_admm_prepare_ex(const admmq_problem* probs, int32_t nprob, int32_t num_attempts,
+                              const admmq_admm_options* opt, void* workspace, size_t workspace_bytes, void* stream);
+/* info[4 p + 3] != 0: an internal fault of problem p (the fused finalize's bounded wait for
+ * its job's selection timed out because the search launch's blocks were not all resident,
+ * e.g. other work on the device). The affected elements were NOT finalized: H_out / U of
+ * that call are invalid and the caller must restore U and re-run with fused_finalize = 0
+ * (the PyTorch op does this itself). */
+int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
+                          int32_t qscheme, int32_t num_attempts, const admmq_admm_options* opt, void* workspace,
+                          size_t workspace_bytes, int32_t* info, void* stream);
 
 /* prepare + run. */
 int32_t admmq_admm_iteration_batched(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps,
@@ -95,6 +127,18 @@ size_t admmq_quantize_workspace_size(const admmq_qtensor* t, int32_t n, int32_t 
 int32_t admmq_quantize_batched(const admmq_qtensor* t, int32_t n, int32_t bits, int32_t qscheme, int32_t num_attempts,
                                void* workspace, size_t workspace_bytes, void* stream);
 
+/* Per-channel schemes with an explicit dim (source/quantization.py:29-33, 91-106):
+ * max / min of every row of unfold(x, dim) (source/utils.py:60-74), then the
+ * tensor_symmetric / tensor_affine arithmetic with those shape[dim] statistics broadcast
+ * against x's LAST dimension as torch does: requires shape[ndim-1] == shape[dim] or one of
+ * them 1 (ADMMQ_ERR_ARG otherwise); y holds shape[:-1] + (max(shape[ndim-1], shape[dim]),)
+ * elements. x contiguous, ndim >= 1, dim in [-ndim, ndim). */
+#define ADMMQ_CHANNEL_SYMMETRIC 4
+#define ADMMQ_CHANNEL_AFFINE 5
+size_t admmq_quantize_channel_workspace_size(const int64_t* shape, int32_t ndim, int32_t dim);
+int32_t admmq_quantize_channel(const float* x, float* y, const int64_t* shape, int32_t ndim, int32_t dim, int32_t bits,
+                               int32_t qscheme, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Canonical SSE table of the MSE-minmax search for one tensor (sse_out: device uint64[num_attempts]). */
 int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t bits, int32_t num_attempts,
                             uint64_t* sse_out, void* workspace, size_t workspace_bytes, void* stream);
@@ -105,12 +149,14 @@ int32_t admmq_mse_sse_table(const float* x, int64_t rows, int64_t cols, int32_t 
  * be the argmin). Both return bit-identical results. */
 int32_t admmq_set_exhaustive_search(int32_t enable);
 
-/* Operand form of the per-iteration solve H_T = P M (the cholesky_solve of
- * source/admm.py:56): 1 (default) = split fp16 planes on f16 MFMA (P and M as
- * hi + lo fp16 with a power-of-two exponent per row, 3 products, fp32 accumulation;
- * about 2^-21 relative per product), 0 = fp32 MFMA. Both stay within the 1e-5
- * rel-Frobenius solve contract of SURVEY.md §8(c) P2. Process-wide; read at
- * admmq_admm_prepare / _run (a prepare and its runs must see the same mode). */
+/* Process default of the per-iteration solve's operand form H_T = P M (the
+ * cholesky_solve of source/admm.py:56) for the plain (non-_ex) entry points:
+ * ADMMQ_SOLVE_FP32 (0, default) = fp32 MFMA, the reference's fp32 arithmetic;
+ * ADMMQ_SOLVE_SPLIT (1) = split fp16 planes on f16 MFMA (P and M as hi + lo fp16 with a
+ * power-of-two exponent per row, 3 products, fp32 accumulation; about 2^-21 relative per
+ * product). Both stay within the 1e-5 rel-Frobenius solve contract of SURVEY.md §8(c) P2.
+ * Read once by admmq_admm_prepare, which records it for its workspace: a later change
+ * does not affect runs on an already prepared workspace. */
 int32_t admmq_set_solve_mode(int32_t mode);
 int32_t admmq_get_solve_mode(void);
 

@@ -195,12 +195,61 @@ def _to_i64(a):
     return out
 
 
+def _trunc_i32_vec(v):
+    v = np.asarray(v, dtype=F32)
+    out = np.where(np.isfinite(v), np.trunc(np.where(np.isfinite(v), v, 0)), 0).astype(np.int64)
+    out[~np.isfinite(v) | (v >= 2.0 ** 31) | (v < -2.0 ** 31)] = -2 ** 31
+    return out
+
+
+def _check_broadcast(shape, nch):
+    """torch broadcasting of the (nch,) channel statistics against the tensor's LAST
+    dimension (the reference divides the tensor by them as they stand)."""
+    last = shape[-1] if len(shape) else 1
+    if last != nch and last != 1 and nch != 1:
+        raise RuntimeError(f"The size of tensor a ({last}) must match the size of tensor b ({nch}) at "
+                           f"non-singleton dimension {max(len(shape) - 1, 0)}")
+
+
+def quantize_channel(x: np.ndarray, bits: int, qscheme: str, dim: int) -> np.ndarray:
+    """``channel_symmetric`` / ``channel_affine`` (``source/quantization.py:29-33, 91-106``):
+    max/min of every row of ``unfold(x, dim)`` (``source/utils.py:60-74``), then the
+    tensor-scheme arithmetic with those (shape[dim],) statistics broadcast against the
+    tensor's last dimension, as torch does (an incompatible size raises RuntimeError)."""
+    x = np.asarray(x, dtype=F32)
+    nd = x.ndim
+    if not -max(nd, 1) <= dim < max(nd, 1):
+        raise IndexError(f"Dimension out of range (expected to be in range of [{-max(nd, 1)}, {max(nd, 1) - 1}], "
+                         f"but got {dim})")
+    d = dim % max(nd, 1)
+    u = np.moveaxis(x.reshape(x.shape if nd else (1,)), d, 0)
+    u = u.reshape(u.shape[0], -1)
+    nch = u.shape[0]
+    _check_broadcast(x.shape, nch)
+    qmax = 2 ** (bits - 1)
+    den = _f32(2 * qmax - 1)
+    with np.errstate(all="ignore"):
+        tmax = u.max(axis=-1).astype(F32)
+        tmin = u.min(axis=-1).astype(F32)
+        if qscheme == "channel_symmetric":
+            m = np.where(np.abs(tmin) > tmax, np.abs(tmin), tmax).astype(F32)
+            scale = ((_f32(2.0) * m).astype(F32) / den).astype(F32)
+            lv = np.clip(np.rint((x / scale).astype(F32)), -qmax, qmax - 1)
+            return (_to_i64(lv).astype(F32) * scale).astype(F32)
+        scale = ((tmax - tmin).astype(F32) / den).astype(F32)
+        zp = (-qmax - _trunc_i32_vec((tmin / scale).astype(F32))).astype(np.int64)
+        zp = ((zp + 2 ** 31) % 2 ** 32 - 2 ** 31)          # int32 wrap (.int())
+        zp = np.clip(zp, -qmax, qmax - 1)
+        lv = np.clip((np.rint((x / scale).astype(F32)) + zp.astype(F32)).astype(F32), -qmax, qmax - 1)
+        return ((_to_i64(lv) - zp).astype(F32) * scale).astype(F32)
+
+
 def quantize_tensor(x: np.ndarray, bits: int, qscheme: str, dim=None, **kwargs) -> np.ndarray:
     """Dispatch of ``source/quantization.py:69-115`` (error behaviour included)."""
     if qscheme in ("channel_symmetric", "channel_affine"):
         if dim is None:
             raise TypeError("channel statistics need a mode (reference: unfold(tensor, None))")
-        raise NotImplementedError("channel schemes are outside the hot path")
+        return quantize_channel(x, bits, qscheme, dim)
     if qscheme == "tensor_symmetric":
         return quantize_symmetric(x, bits)
     if qscheme == "tensor_affine":

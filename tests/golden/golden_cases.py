@@ -132,3 +132,46 @@ def level_mismatch(H, H_ref, X, half_window=1e-4):
     y = np.asarray(X, np.float64) / np.float64(s)
     near = np.abs(np.abs(y - np.floor(y)) - 0.5) < half_window
     return int(bad.sum()), int((bad & ~(near & (np.abs(k - kr) == 1))).sum())
+
+
+# F9: per-channel quantizers with an explicit dim (source/quantization.py:29-33, 91-106).
+# The per-channel stats (shape (shape[dim],)) broadcast against the tensor's LAST dimension
+# (torch broadcasting), so a dim other than the last works only when the sizes agree (or
+# one is 1) - otherwise the reference raises RuntimeError. Kept as the reference does it.
+F9_LAYOUTS = [
+    ((64, 134), 1), ((64, 134), 0), ((64, 64), 0), ((16, 8, 9), 2), ((9, 8, 9), 0), ((5, 1), 0),
+    ((100,), 0), ((16, 8, 9), -1), ((7, 3, 4), 1), ((1, 1), 0), ((1, 1), 1), ((12, 1, 3), 1),
+]
+
+
+def f9_cases():
+    cases = []
+    seed = 9000
+    for shape, dim in F9_LAYOUTS:
+        for qs in ("channel_symmetric", "channel_affine"):
+            for bits, scale in ((4, 1.0), (2, 1e-3), (8, 0.05)):
+                seed += 1
+                cases.append(dict(id=f"k{seed:05d}", kind="randn", shape=list(shape), dim=dim, scale=scale,
+                                  bits=bits, qscheme=qs, seed=seed))
+    # constant / zero / NaN / inf channels (scale 0, NaN stats; torch's x86 conversions)
+    for kind in ("constcol", "nancol", "infcol"):
+        for qs in ("channel_symmetric", "channel_affine"):
+            seed += 1
+            cases.append(dict(id=f"k{seed:05d}", kind=kind, shape=[6, 10], dim=1, scale=1.0, bits=4, qscheme=qs,
+                              seed=seed))
+    return cases
+
+
+def f9_input(case) -> np.ndarray:
+    shape = tuple(case["shape"])
+    rng = np.random.default_rng(case["seed"])
+    x = rng.standard_normal(shape) * case["scale"]
+    if case["kind"] == "constcol":
+        x[:, 3] = 0.75
+        x[:, 6] = 0.0
+    elif case["kind"] == "nancol":
+        x[2, 4] = np.nan
+    elif case["kind"] == "infcol":
+        x[1, 7] = np.inf
+        x[4, 2] = -np.inf
+    return x.astype(np.float32)

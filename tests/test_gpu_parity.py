@@ -417,3 +417,91 @@ def test_fused_finalize_equals_separate(torch_dev, eps):
         assert np.array_equal(ia, ib)
         for (ha, ua), (hb, ub) in zip(a, b):
             assert _bits_equal(ha, hb) and _bits_equal(ua, ub)
+
+
+def test_fused_finalize_timeout_reported_and_repaired(torch_dev):
+    """A fused-finalize block whose bounded wait for its job's selection times out (forced
+    here: one poll) must not finalize with a stale selection: the C-ABI run reports it in
+    info[:, 3] and leaves those elements alone; the torch op (and the ctypes route)
+    restore U and re-run with the separate finalize launch, so the caller gets exactly the
+    bits of an undisturbed run."""
+    import ctypes
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    from admmq.admm import _admm_iteration_batched_cabi, _problem
+    probs_np = [_layer_problem(l, m) for l, m in [("layer4.1.conv2", 0), ("layer3.1.conv2", 1), ("layer1.0.conv1", 0)]]
+
+    def mk():
+        return [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+                for H, F, G in probs_np]
+
+    ref_ps = mk()
+    with _lib.fused_finalize(False):
+        ref_H, ref_info = admm_iteration_batched(ref_ps, 8, 0.0, 4, MSE, return_info=True)
+    ref = [(h.cpu().numpy(), p[1].cpu().numpy()) for h, p in zip(ref_H, ref_ps)]
+
+    # the raw C-ABI run reports the fault
+    lib = _lib.load()
+    ps = mk()
+    items = [_problem(H, U, F, G) for H, U, F, G in ps]
+    outs = [torch.empty_like(p[0]) for p in ps]
+    for it, o in zip(items, outs):
+        it.H_out = o.data_ptr()
+    arr = _lib.problems_array(items)
+    opt = _lib.default_options()
+    opt.solve_mode = 0
+    opt.fused_finalize = 1
+    po = ctypes.byref(opt)
+    nb = lib.admmq_admm_workspace_size_ex(arr, len(items), 200, po)
+    ws = _lib.workspace(nb, dev)
+    st = _lib.stream_handle(dev)
+    info = torch.zeros(len(items) * 4, dtype=torch.int32, device=dev)
+    _lib.check(lib.admmq_admm_prepare_ex(arr, len(items), 200, po, _lib.ptr(ws), nb, st), "prepare")
+    with _lib.fin_wait_polls(1):
+        _lib.check(lib.admmq_admm_run_ex(arr, len(items), 8, 0.0, 4, 0, 200, po, _lib.ptr(ws), nb, _lib.ptr(info), st),
+                   "run")
+    torch.cuda.synchronize()
+    assert int(info.view(-1, 4)[:, 3].max()) != 0, "a one-poll wait should have timed out somewhere"
+    # a run must ask for the mode its prepare recorded
+    opt2 = _lib.default_options()
+    opt2.solve_mode = 1
+    assert lib.admmq_admm_run_ex(arr, len(items), 8, 0.0, 4, 0, 200, ctypes.byref(opt2), _lib.ptr(ws), nb,
+                                 _lib.ptr(info), st) != 0
+
+    # both routes repair it
+    for route in ("ops", "cabi"):
+        ps = mk()
+        with _lib.fin_wait_polls(1):
+            if route == "ops":
+                Hs, inf = admm_iteration_batched(ps, 8, 0.0, 4, MSE, return_info=True)
+            else:
+                Hs, inf = _admm_iteration_batched_cabi(ps, 8, 0.0, 4, 0, 200, False, False, True)
+        assert int(inf[:, 3].max()) == 0
+        for (hr, ur), h, p in zip(ref, Hs, ps):
+            assert _bits_equal(hr, h.cpu().numpy()) and _bits_equal(ur, p[1].cpu().numpy())
+
+
+@pytest.mark.parametrize("route", ["ops", "cabi"])
+def test_channel_schemes_reference_kats(torch_dev, route, monkeypatch):
+    """channel_symmetric / channel_affine with an explicit dim on the device
+    (admmq_quantize_channel): bit-exact with every reference output of F9 (shape included)
+    and the reference's RuntimeError where the statistics do not broadcast."""
+    torch, dev = torch_dev
+    from admmq import quantize_tensor, _lib
+    if route == "cabi":
+        monkeypatch.setattr(_lib, "use_ops", lambda: False)
+    with open(os.path.join(GOLDEN, "f9_channel.json")) as f:
+        meta = json.load(f)["cases"]
+    bad = []
+    for case in meta:
+        x = _t(torch, dev, gc.f9_input(case))
+        if case["error"] is not None:
+            with pytest.raises(RuntimeError, match="must match the size"):
+                quantize_tensor(x, case["bits"], case["qscheme"], dim=case["dim"])
+            continue
+        y = quantize_tensor(x, case["bits"], case["qscheme"], dim=case["dim"]).cpu().numpy()
+        if list(y.shape) != case["out_shape"] or gc.canonical_sha(y) != case["sha"]:
+            bad.append(case["id"])
+    assert bad == [], f"{len(bad)} of {len(meta)} F9 KATs differ: {bad}"
+    with pytest.raises(TypeError):
+        quantize_tensor(_t(torch, dev, gc.f9_input(meta[0])), 4, "channel_symmetric")

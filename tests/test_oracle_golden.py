@@ -95,3 +95,28 @@ def test_f8_reference_branches_pin_f2_and_oracle():
         H, _ = ao.admm_iteration(H0, np.zeros_like(H0), F, G, 6, 1e-8, 4, qs)
         _, s = gc.grid_levels(H)
         assert any(abs(float(s) - b["scale"]) / b["scale"] < 1e-5 for b in c["branches"]), (c["key"], float(s))
+
+
+def _load_f9():
+    with open(os.path.join(GOLDEN, "f9_channel.json")) as f:
+        return json.load(f)["cases"], np.load(os.path.join(GOLDEN, "f9_channel.npz"))
+
+
+def test_f9_channel_kats():
+    """channel_symmetric / channel_affine with an explicit dim: the oracle reproduces every
+    reference output of F9 bit for bit (shape included: the statistics broadcast against
+    the last dimension) and raises the reference's error, with its message, where it raises."""
+    meta, arrays = _load_f9()
+    assert len(meta) == 78
+    for case in meta:
+        x = gc.f9_input(case)
+        if case["error"] is not None:
+            with pytest.raises(RuntimeError) as ei:
+                qo.quantize_tensor(x, case["bits"], case["qscheme"], dim=case["dim"])
+            assert type(ei.value).__name__ == case["error"] and str(ei.value) == case["message"]
+            continue
+        y = qo.quantize_tensor(x, case["bits"], case["qscheme"], dim=case["dim"])
+        assert list(y.shape) == case["out_shape"], case["id"]
+        assert _sha(y) == case["sha"], case["id"]
+        ref = arrays[case["id"]]
+        assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])

@@ -14,10 +14,11 @@ from conftest import gpu_available
 SCHEMAS = {
     "admm_iteration_batched": "admmq::admm_iteration_batched(Tensor[] H, Tensor(a!)[] U, Tensor[] F, Tensor[] G, "
                               "int max_iter, float eps, int bits, int qscheme, int num_attempts=200, "
-                              "bool check_spd=True, bool debug=False) -> (Tensor[] H_out, Tensor info, Tensor[] HT, "
+                              "bool check_spd=True, bool debug=False, int solve=-1) -> (Tensor[] H_out, Tensor info, Tensor[] HT, "
                               "Tensor[] X)",
     "quantize_batched": "admmq::quantize_batched(Tensor[] x, int bits, int qscheme, int num_attempts=200, "
                         "float? tmin=None, float? tmax=None) -> Tensor[]",
+    "quantize_channel": "admmq::quantize_channel(Tensor x, int bits, int qscheme, int dim) -> Tensor",
     "cp_gram_mttkrp": "admmq::cp_gram_mttkrp(Tensor[] W, Tensor[] factors, int mode) -> (Tensor[] G, Tensor[] F)",
     "cp_rel_error": "admmq::cp_rel_error(Tensor[] W, Tensor[] factors) -> Tensor",
 }

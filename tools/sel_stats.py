@@ -14,7 +14,7 @@ import bench  # noqa: E402
 
 lib = _lib.load()
 buf = (ctypes.c_ulonglong * 3)()
-work = bench.build_workload("resnet18", 0, 1, "replica", torch.device("cuda:0"))
+work, _, _ = bench.build_workload("resnet18", 0, 1, "replica", torch.device("cuda:0"))
 lib.admmq_debug_sel_stats(buf, 1)
 bench.run_step(work, int(sys.argv[1]) if len(sys.argv) > 1 else 1000)
 torch.cuda.synchronize()

@@ -87,7 +87,7 @@ def _problem(H, U, F, G, HT_out=None, X_out=None):
 def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]],
                            max_iter: int, eps: float, bits: int, qscheme: str, num_attempts: int = 200,
                            check_spd: bool = True, debug_outputs: bool = False, return_info: bool = False,
-                           solve: Optional[str] = None):
+                           solve: Optional[str] = None, check_fault: bool = True):
     """Run ``admm_iteration`` on every (H, U, F, G) of ``problems`` in shared launches.
 
     Returns the list of new H tensors (and the caller's U tensors are updated in
@@ -98,8 +98,13 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     or ``"split"`` for this call. Calls ``torch.ops.admmq.admm_iteration_batched``
     (csrc/torch_ops.cpp), which calls ``admmq_admm_prepare_ex`` / ``admmq_admm_run_ex``;
     an internal fault of the fused finalize (its bounded wait timed out) is repaired
-    inside the call by a re-run with the separate finalize launch.
+    inside the call by a re-run with the separate finalize launch (one host sync per call).
+    ``check_fault=False`` skips that sync (calls on several streams can then overlap): the
+    caller must read ``info[:, 3]`` itself and repeat the call with ``U`` restored where it
+    is nonzero (``return_info`` is then required).
     """
+    if not check_fault and not return_info:
+        raise ValueError("check_fault=False needs return_info=True (the caller must check info[:, 3])")
     solve_code = -1 if solve is None else _lib.SOLVE_MODES[solve]
     if len(problems) == 0:
         return []
@@ -110,11 +115,11 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     code = _scheme_code(qscheme)
     if not _lib.use_ops():
         return _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd,
-                                            debug_outputs, return_info, solve_code)
+                                            debug_outputs, return_info, solve_code, check_fault)
     Hs, Us, Fs, Gs = (list(x) for x in zip(*problems))
     outs, info, hts, xs = _lib.ops().admm_iteration_batched(Hs, Us, Fs, Gs, int(max_iter), float(eps), int(bits), code,
                                                             int(num_attempts), bool(check_spd), bool(debug_outputs),
-                                                            solve_code)
+                                                            solve_code, bool(check_fault))
     ret = [list(outs) if max_iter > 1 else [p[0] for p in problems]]   # max_iter <= 1: the input H objects
     if debug_outputs:
         ret.append(list(zip(hts, xs)))
@@ -124,7 +129,7 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
 
 
 def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attempts, check_spd, debug_outputs,
-                                 return_info, solve_code=-1):
+                                 return_info, solve_code=-1, check_fault=True):
     """The same call through the C-ABI with ctypes (diagnostic builds, cross-checks),
     including the op's internal-fault repair (restore U, re-run without the fused finalize)."""
     import ctypes
@@ -164,14 +169,14 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
     for it, o in zip(items, outs):
         it.H_out = o.data_ptr()
     arr = _lib.problems_array(items)
-    ubak = [u.clone() for u in Us]
+    ubak = [u.clone() for u in Us] if check_fault else []
 
     def run():
         _lib.check(lib.admmq_admm_run_ex(arr, n, int(max_iter), float(eps), int(bits), code, int(num_attempts), po,
                                          _lib.ptr(ws), nb, _lib.ptr(info), stream), "admm_run")
 
     run()
-    if int(info.view(n, 4)[:, 3].max().item()) != 0:   # internal fault: repeat without the fused finalize
+    if check_fault and int(info.view(n, 4)[:, 3].max().item()) != 0:   # internal fault: repeat without the fused finalize
         for u, b in zip(Us, ubak):
             u.copy_(b)
         opt.fused_finalize = 0

@@ -11,9 +11,10 @@ rho, max_iter, eps)`` (``:85-101``) with the other part held fixed.
   every ``poll`` iterations to stop queueing early.
 * The quantization projection is the HIP quantizer (``admmq.quantize_tensor``).
 * The rank projection is ``project_rank`` (exact truncated SVD, the reference's
-  semantics) or ``SubspaceProjector``: a warm-started block subspace iteration that
-  converges to the same truncation (top-``rank`` singular triplets) with a few thin
-  GEMMs per call instead of a full SVD of a 4096 x 11008 matrix.
+  semantics), ``KrylovProjector`` (warm-started block Krylov in float64 that stops at a
+  residual bound: agrees with the exact truncation to ~1e-4 also on the flat spectra of
+  the loop's iterates) or ``SubspaceProjector`` (warm-started subspace iteration: cheaper,
+  but it stalls on flat spectra - kept for comparison).
 """
 from __future__ import annotations
 
@@ -74,6 +75,71 @@ class SubspaceProjector:
         return Ur @ torch.diag(S[:r]) @ Vt[:r]
 
 
+class KrylovProjector:
+    """Rank-``rank`` truncation that matches the exact SVD truncation of
+    ``project_rank`` (``scripts/factorize_lowrank.py:80-82``) to ``tol`` on the loop's own
+    iterates, including the flat spectra of the low-rank ADMM (sigma_r / sigma_{r+1} ~
+    1 + 1e-3 for a 4096 x 4096 noise-like target), where plain subspace iteration stalls.
+
+    Block Krylov (randomized block Lanczos, full re-orthogonalization) in float64 on the
+    device: K = [Q, (X X^T) Q, (X X^T)^2 Q, ...] with blocks of ``block`` columns, warm-started
+    from the previous call's Ritz vectors; every ``check_every`` blocks a Rayleigh-Ritz
+    step (eigh of B B^T, B = K^T X) gives the top-``rank`` triplets (sigma_i, u_i, v_i with
+    X^T u_i = sigma_i v_i exactly) and the residuals ||X v_i - sigma_i u_i|| / sigma_1; it
+    stops when the largest is <= ``tol`` (the truncation then agrees with the exact one to
+    about 2 ``tol`` relative: measured on flat spectra, tools/lowrank_bench.py reports it).
+    The products are GEMMs of the tall operand with ``block``-wide panels (hipBLASLt)."""
+
+    def __init__(self, rank: int, block: int = 32, tol: float = 2e-5, check_every: int = 4, max_blocks: int = 64,
+                 seed: int = 0):
+        self.rank, self.block, self.tol = rank, block, tol
+        self.check_every, self.max_blocks, self.seed = check_every, max_blocks, seed
+        self.Q: Optional[torch.Tensor] = None
+        self.blocks: List[int] = []
+        self.residuals: List[float] = []
+
+    def __call__(self, X: torch.Tensor) -> torch.Tensor:
+        m, n = X.shape
+        r = min(self.rank, m, n)
+        k = min(self.block, m, n)
+        Xd = X.double()
+        if self.Q is None or self.Q.shape != (m, k):
+            g = torch.Generator().manual_seed(self.seed)
+            self.Q = torch.linalg.qr(Xd @ torch.randn(n, k, generator=g, dtype=torch.float64).to(X.device))[0]
+        blocks = [self.Q]
+        K = self.Q
+        Q = self.Q
+        res = float("inf")
+        nb = 1
+        while True:
+            if nb >= self.max_blocks or K.shape[1] + k > min(m, n):
+                do_check = True
+            else:
+                Z = Xd @ (Xd.T @ Q)
+                for _ in range(2):   # full re-orthogonalization against every block so far
+                    Z = Z - K @ (K.T @ Z)
+                Q = torch.linalg.qr(Z)[0]
+                blocks.append(Q)
+                K = torch.cat(blocks, 1)
+                nb += 1
+                do_check = nb % self.check_every == 0
+            if not do_check:
+                continue
+            B = K.T @ Xd                                   # (nb k) x n
+            evals, evecs = torch.linalg.eigh(B @ B.T)      # ascending
+            idx = torch.arange(evals.shape[0] - 1, evals.shape[0] - 1 - max(k, r), -1, device=X.device)
+            S = torch.sqrt(torch.clamp(evals[idx], min=0.0))
+            Ub = evecs[:, idx]
+            U = K @ Ub[:, :r]
+            V = (B.T @ Ub[:, :r]) / S[:r]
+            res = float(torch.max(torch.linalg.norm(Xd @ V - U * S[:r], dim=0)) / S[0])
+            if res <= self.tol or nb >= self.max_blocks or K.shape[1] + k > min(m, n):
+                self.Q = torch.linalg.qr(K @ Ub[:, :k])[0]   # warm start: the leading Ritz vectors
+                self.blocks.append(nb)
+                self.residuals.append(res)
+                return ((U * S[:r]) @ V.T).to(X.dtype)
+
+
 def _is_device_quantizer(f) -> bool:
     return isinstance(f, partial) and f.func is quantize_tensor
 
@@ -131,7 +197,8 @@ def factorize_lowrank(W: torch.Tensor, bits: int, rank: int, qscheme: str = "ten
     dev = W.device
     g = torch.Generator().manual_seed(seed)
     quant = partial(quantize_tensor, qscheme=qscheme, bits=bits)
-    proj = partial(project_rank, rank=rank) if projection == "svd" else SubspaceProjector(rank, seed=seed)
+    proj = (partial(project_rank, rank=rank) if projection == "svd" else
+            KrylovProjector(rank, seed=seed) if projection == "krylov" else SubspaceProjector(rank, seed=seed))
     W_q = torch.randn(*W.shape, generator=g).to(dev)
     U_q = torch.zeros_like(W_q)
     W_r = proj(torch.randn(*W.shape, generator=g).to(dev))
@@ -167,7 +234,7 @@ def main(argv=None):
     ap.add_argument("--qscheme", type=str, default="tensor_minmax")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--weights", type=str, default=None)
-    ap.add_argument("--projection", choices=["svd", "subspace"], default="svd")
+    ap.add_argument("--projection", choices=["svd", "krylov", "subspace"], default="svd")
     a = ap.parse_args(argv)
     if not torch.cuda.is_available():
         raise RuntimeError("admmq.lowrank needs a ROCm GPU")

@@ -111,7 +111,7 @@ struct QJob {
 // tile entry only, not on a further descriptor read. Split form: P / M point at the
 // fp16 planes (row strides in floats are unchanged), eP / eM at the row exponents.
 struct GemmTile {
-  int prob, tm, tn, first, nk, pad_;
+  int prob, tm, tn, first, nk, bm;   // bm: tile rows of the persistent fp32 kernel (k_gemm_f32p), else 0
   const float* P; const float* M; const float* U;
   const int* eP; const int* eM;
   int ld, ldm;
@@ -187,6 +187,8 @@ void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int 
                       int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s);
+void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
+                      float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,

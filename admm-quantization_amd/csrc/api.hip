@@ -77,6 +77,90 @@ static std::atomic<int> g_hist_reps{0};
 // shrink it to force the timeout path)
 static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
 
+// Tile rows of the persistent fp32 solve per problem (fixed by the problem's shape, never
+// by the batch, so every element's result is batch-independent): 0 = 64 x 64 tiles
+// (32-row factors: 32 x 64); 1 = 128 x 64 tiles for the factors with ld >= 1024 whose I
+// is a multiple of 128, 32 x 64 tiles for the others (finer filler tiles: the CU-level
+// LPT of a launch then balances to ~0.99 at C3 instead of 0.89, where the 36-K-step 64 x 64
+// tiles of the R = 1141 layers left gaps only coarse tiles could not fill); 2 = 64 x 64 for
+// ld >= 1024, 32 x 64 for the others; 3 = 128 x 64 for ld >= 1024, 64 x 64 for the others.
+static std::atomic<int> g_f32_rule{1};
+static std::atomic<bool> g_f32p{false};  // persistent fp32 solve (diagnostics: slower than k_gemm)
+static int f32_tile_rows(int I, int ld) {
+  if (I <= 32) return 32;
+  const int rule = g_f32_rule.load();
+  const bool big = ld >= 1024;
+  switch (rule) {
+    case 0: return 64;
+    case 2: return big ? 64 : 32;
+    case 3: return (big && I % 128 == 0) ? 128 : 64;
+    default: return (big && I % 128 == 0) ? 128 : 32;
+  }
+}
+static constexpr int kF32Slots = 2;   // k_gemm_f32p workgroups per CU (72 KB of LDS each)
+
+// CUs of the current device (looked up once per device)
+static int device_cus() {
+  constexpr int kMaxDev = 64;
+  static std::once_flag once[kMaxDev];
+  static int cus[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+  std::call_once(once[dev], [dev]() {
+    int n = 0;
+    cus[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+  });
+  return cus[dev];
+}
+
+// Persistent fp32 solve lists: every tile goes, largest MFMA work first, to the CU with the
+// least work so far (ties: the CU whose XCD already holds tiles of the same M column / P row
+// panel, which then come from that XCD's L2), then each CU's tiles are split over its
+// kF32Slots workgroups (LPT again). Workgroup b runs on CU b mod ncu (round-robin dispatch;
+// a different placement only costs speed). Fills `tiles` in list order and `off`.
+static void plan_f32_lists(std::vector<GemmTile>& tiles, std::vector<int>& off, int ncu) {
+  std::vector<GemmTile> sorted = tiles;
+  auto work = [](const GemmTile& t) { return (long long)t.bm * t.nk; };
+  std::stable_sort(sorted.begin(), sorted.end(), [&](const GemmTile& a, const GemmTile& b) { return work(a) > work(b); });
+  constexpr int kXcd = 8;
+  std::vector<std::vector<GemmTile>> bins(ncu);
+  std::vector<long long> load(ncu, 0);
+  std::map<std::pair<int, int>, std::array<int, kXcd>> col_on, row_on;
+  for (const GemmTile& t : sorted) {
+    auto& cx = col_on[{t.prob, t.tn}];
+    auto& rx = row_on[{t.prob, t.tm * t.bm}];
+    int best = 0;
+    long long best_key = 0;
+    for (int b = 0; b < ncu; ++b) {
+      const long long key = load[b] * 1000000LL - cx[b % kXcd] * 1000LL - rx[b % kXcd];
+      if (b == 0 || key < best_key) { best = b; best_key = key; }
+    }
+    bins[best].push_back(t);
+    load[best] += work(t);
+    cx[best % kXcd] += 1;
+    rx[best % kXcd] += 1;
+  }
+  const int nslots = ncu * kF32Slots;
+  std::vector<std::vector<GemmTile>> lists(nslots);
+  for (int c = 0; c < ncu; ++c) {
+    long long sl[kF32Slots] = {};
+    for (const GemmTile& t : bins[c]) {   // already largest first
+      int k = 0;
+      for (int j = 1; j < kF32Slots; ++j)
+        if (sl[j] < sl[k]) k = j;
+      lists[c + (size_t)k * ncu].push_back(t);
+      sl[k] += work(t);
+    }
+  }
+  tiles.clear();
+  off.assign(nslots + 1, 0);
+  for (int b = 0; b < nslots; ++b) {
+    off[b] = (int)tiles.size();
+    tiles.insert(tiles.end(), lists[b].begin(), lists[b].end());
+  }
+  off[nslots] = (int)tiles.size();
+}
+
 // Solve mode recorded by each prepare for its workspace (the run must use the operand
 // planes its prepare wrote: the per-problem buffer carve depends on the mode).
 static std::mutex g_ws_mu;
@@ -193,6 +277,11 @@ struct AdmmPlan {
   size_t bytes = 0;
   int maxIp = 0, maxld = 0, maxldm = 0, maxnbk = 0, maxI = 0, maxR = 0;
   int ntiles_wide = 0, ntiles_big = 0, ntiles_small = 0;   // 256x128, 64x64, 32x64 tiles (in that order)
+  // persistent fp32 solve (k_gemm_f32p): tiles in list order, workgroup b's list [off[b], off[b+1])
+  bool f32p = false;
+  std::vector<int> list_off;
+  int* d_list_off = nullptr;
+  int nslots = 0;
   bool wide = false;                                       // I > 64 factors take 256x128 tiles (k_gemm<8, 1, 3, *, 2>)
   int fin_groups = 1;             // float4 groups per thread of the finalize units
   int hist_nv = 1;
@@ -206,7 +295,7 @@ struct AdmmPlan {
 
 static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
   GemmTile t;
-  t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.nk = nk; t.pad_ = 0;
+  t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.nk = nk; t.bm = 0;
   t.P = nullptr; t.M = nullptr; t.U = nullptr; t.eP = nullptr; t.eM = nullptr; t.ld = 0; t.ldm = 0;   // set at upload
   return t;
 }
@@ -297,7 +386,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? kWideRows : 64);
+    const bool f32p_prob = !pl.split && g_f32p.load() && !(pl.wide && a.I > 64) && a.I > kThinRows;
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? kWideRows : (f32p_prob ? std::max(64, f32_tile_rows(a.I, rup(a.R, 32))) : 64));
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -378,8 +468,34 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       wide.push_back(q[x][head[x]++]);
     }
   }
+  // persistent fp32 solve: every non-thin, non-wide factor in per-workgroup lists
+  pl.f32p = !pl.split && g_f32p.load();
+  pl.list_off.clear();
+  pl.nslots = 0;
+  if (pl.f32p) {
+    std::vector<GemmTile> ft;
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if (d.I <= kThinRows || (pl.wide && d.I > 64)) continue;
+      const int bm = f32_tile_rows(d.I, d.ld);
+      const int TM = (d.I + bm - 1) / bm, TN = (d.ld + 63) / 64;
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = 0; tn < TN; ++tn) {
+          GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32);
+          t.bm = bm;
+          ft.push_back(t);
+        }
+    }
+    if (!ft.empty()) {
+      const int ncu = device_cus();
+      plan_f32_lists(ft, pl.list_off, ncu);
+      pl.nslots = ncu * kF32Slots;
+    }
+    pl.tiles = ft;   // the wide tiles (if any) are inserted in front below
+  }
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
+    if (pl.f32p) break;
     if (d.I <= kThinRows || d.Ip == 32 || (pl.wide && d.I > 64)) continue;   // thin / 32-row / wide: elsewhere
     const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
     for (int g0 = 0; g0 < TN; g0 += 8)
@@ -387,15 +503,16 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
         for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
           pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
   }
-  order_tiles_for_cus(pl.tiles, 256, 3);
+  if (!pl.f32p) order_tiles_for_cus(pl.tiles, 256, 3);
   std::vector<GemmTile> small;
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
+    if (pl.f32p) break;
     if (d.I <= kThinRows || d.Ip != 32) continue;
     const int TN = (d.ld + 63) / 64;
     for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
   }
-  pl.ntiles_big = (int)pl.tiles.size();
+  pl.ntiles_big = pl.f32p ? 0 : (int)pl.tiles.size();   // f32p: the tiles after the wide ones are list-ordered
   pl.ntiles_small = (int)small.size();
   pl.ntiles_wide = (int)wide.size();
   pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
@@ -489,6 +606,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i = 0; i < nprob; ++i) pl.desc[i].mv.ready = pl.d_ready ? pl.d_ready + 2 * i : nullptr;
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
+  pl.d_list_off = cv.take<int>(pl.list_off.size() + 1);
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
@@ -518,6 +636,8 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
     }
   }
   if ((rc = h2d(pl.d_tiles, pl.tiles.data(), pl.tiles.size() * sizeof(GemmTile), s))) return rc;
+  if (!pl.list_off.empty() && (rc = h2d(pl.d_list_off, pl.list_off.data(), pl.list_off.size() * sizeof(int), s)))
+    return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
@@ -692,6 +812,15 @@ int32_t admmq_debug_set_fin_wait_polls(uint32_t polls) {
   return ADMMQ_OK;
 }
 
+// diagnostics (not in include/admmq.h): persistent fp32 solve on/off and its tile rule
+// (f32_tile_rows; changes the bits of the factors whose tile rows change between 64 and 32)
+int32_t admmq_debug_set_f32_persistent(int32_t enable, int32_t rule) {
+  if (rule < 0 || rule > 3) return fail(ADMMQ_ERR_ARG, "rule must be 0..3");
+  g_f32p = enable != 0;
+  g_f32_rule = rule;
+  return ADMMQ_OK;
+}
+
 // diagnostics (not in include/admmq.h): 1 = per-level stage 1, 0 = merged thresholds
 int32_t admmq_debug_set_legacy_stage1(int32_t enable) {
   g_legacy_stage1 = enable != 0;
@@ -845,10 +974,14 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
-    if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0) {
+    if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big + pl.nslots > 0) {
       prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
-      launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
-                  num_attempts, s);
+      if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0)
+        launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
+                    num_attempts, s);
+      if (pl.nslots > 0)
+        launch_gemm_f32p(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.d_list_off, pl.nslots, slot, it, eps, num_attempts,
+                         s);
       prof_mark(s);
     }
     if (!pl.thin.empty()) {

@@ -320,6 +320,210 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent fp32 solve (kSolveF32, launches without wide tiles): kF32Slots workgroups
+// per CU, workgroup b runs the tiles list[off[b] .. off[b+1]) one after another. The host
+// (api.hip: plan_f32_lists) places the tiles by LPT over the CUs on their MFMA work
+// (workgroups b and b + ncu share CU b, round-robin dispatch; placement is only for
+// speed), so a launch's length is set by the CU total rather than by how the largest
+// tiles happen to land. Tile shapes (fixed per problem, so every element's result is
+// independent of the batch):
+//   BM 128 x 64  (4 waves of 32 x 64: one A fragment feeding two accumulators)
+//   BM  64 x 64  (2 x 2 waves of 32 x 32)          - the same MFMA chain per element as
+//   BM  32 x 64  (2 waves of 32 x 32 x 2 K-halves)   k_gemm<2,1,..> / k_gemm<1,2,..>
+// Every element's MFMA sequence (k = 16 h + 4 qq + j per K-step, KS = 1) is the one of
+// the 64 x 64 tiles, so BM 128 and BM 64 give identical bits; BM 32 sums two K-halves
+// like k_gemm<1, 2, ..>. Staging as k_gemm: K-step 32, LDS-DMA into an NS-deep ring of
+// (128 + 64)-row stages (the rows of smaller tiles use the front of each stage).
+template <int BM, int NS>
+__device__ __forceinline__ void f32_tile(const ProbDesc* __restrict__ probs, const GemmTile& tl, int slot, int iter,
+                                         float eps, int ncand, float* const (&stp)[4], unsigned (*red)[4]) {
+  constexpr int CW = BM == 128 ? 2 : 1;           // 32-column accumulators per wave
+  constexpr int NSUB = (BM / 32) * (2 / CW);      // sub-tiles (waves per K-slice)
+  constexpr int KS = 4 / NSUB;                    // K-slices
+  constexpr int QS = 4 / KS;                      // b128 fragment reads per operand per wave per K-step
+  constexpr int ROWS = BM + 64;                   // image rows per stage (A then B)
+  constexpr int NG = ROWS / 8;                    // glds wave-instructions per stage
+  constexpr int GPW = NG / 4;                     // ... per wave
+  static_assert(NG % 4 == 0 && GPW * (NS - 2) < 64, "stage split");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = wave % NSUB, ks = wave / NSUB;
+  const int wm = sub / (2 / CW), wn = sub % (2 / CW);
+  const int i = lane & 31, h = lane >> 5;
+  const int swz = (i >> 1) & 7;
+  const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * CW * wn + i) * 32;   // sub-tile c: boff + 1024 c
+  const ProbDesc& p = probs[tl.prob];
+  const int ld = tl.ld, ldm = tl.ldm;
+  const int row0 = tl.tm * BM, col0 = tl.tn * 64;
+  const int nk = tl.nk;
+  // the epilogue's U entries, loaded first (their latency is spent under the K-loop)
+  float upre[CW][16];
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int col = col0 + 32 * (CW * wn + c) + i;
+    const int colc = col < ld ? col : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      upre[c][r] = ldg(tl.U + (size_t)row * ld + colc);
+    }
+  }
+  const float* src[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int g = wave * GPW + j;
+    const int r = 8 * g + (lane >> 3);                       // image row
+    const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+    src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + 4 * c
+                      : tl.M + (size_t)min(col0 + r - BM, ldm - 1) * ldm + 4 * c;
+  }
+#define ADMMQ_ISSUE(s, kt)                                                 \
+  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
+    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
+  bool skip = p.flags[0] != 0;
+  if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
+    if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
+    skip = true;
+  }
+  if (skip) {
+    wait_vmcnt<0>();   // the speculative stage loads land before the stages are reused
+    return;
+  }
+  if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+    unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
+    unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
+    unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
+    for (int c = tid; c < ncand; c += 256) sse[c] = 0ull;
+    for (int c = tid; c < kHistRep * (ncand + 1); c += 256) { h1[c] = 0ull; h2[c] = 0ull; }
+    if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
+  }
+  f32x16 acc[CW];
+#pragma unroll
+  for (int c = 0; c < CW; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+#define ADMMQ_STEP(s, kt)                                                                     \
+  do {                                                                                        \
+    wait_vmcnt<GPW * (NS - 2)>();                                                             \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
+    raw_barrier();                                                                            \
+    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
+    const float* st = stp[s];                                                                 \
+    _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                       \
+      const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                                    \
+      const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);                    \
+      float4 b[CW];                                                                           \
+      _Pragma("unroll") for (int c = 0; c < CW; ++c)                                          \
+        b[c] = *reinterpret_cast<const float4*>(st + boff + 1024 * c + cpos);                 \
+      _Pragma("unroll") for (int c = 0; c < CW; ++c)                                          \
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[c].x, acc[c], 0, 0, 0);          \
+      _Pragma("unroll") for (int c = 0; c < CW; ++c)                                          \
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[c].y, acc[c], 0, 0, 0);          \
+      _Pragma("unroll") for (int c = 0; c < CW; ++c)                                          \
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[c].z, acc[c], 0, 0, 0);          \
+      _Pragma("unroll") for (int c = 0; c < CW; ++c)                                          \
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[c].w, acc[c], 0, 0, 0);          \
+    }                                                                                         \
+  } while (0)
+  const int nfull = nk / NS * NS;
+  for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ADMMQ_STEP(s, kt0 + s);
+  }
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (nfull + s < nk) ADMMQ_STEP(s, nfull + s);
+#undef ADMMQ_STEP
+#undef ADMMQ_ISSUE
+  __syncthreads();   // nothing in flight any more; the stages may be reused
+  if (KS > 1) {      // fixed-order reduction of the K-slice partial accumulators (deterministic)
+    if (ks > 0) {
+      float* dst = stp[0] + ((ks - 1) * NSUB + sub) * 1024;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[0][r];
+    }
+    __syncthreads();
+    if (ks == 0) {
+#pragma unroll
+      for (int j = 1; j < KS; ++j) {
+        const float* s2 = stp[0] + ((j - 1) * NSUB + sub) * 1024;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][r] += s2[r * 64 + lane];
+      }
+    }
+  }
+  // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if (ks == 0) {
+    unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+    typedef __attribute__((address_space(1))) float gf32;
+    gf32* const HTg = (gf32*)p.HT;
+    gf32* const Xg = p.X_dbg ? (gf32*)p.X : nullptr;   // X = H_T - U is re-formed by its readers; debug output only
+    const int pI = p.I, pR = p.R;
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+      const int col = col0 + 32 * (CW * wn + c) + i;
+      if (col < ld) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const size_t off = (size_t)row * ld + col;
+          const float ht = acc[c][r];
+          const float x = ht - upre[c][r];
+          HTg[off] = ht;
+          if (Xg) Xg[off] = x;
+          if (row < pI && col < pR) {
+            amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
+            const unsigned e = enc_ord(x);
+            mn = min(mn, e);
+            mxo = max(mxo, e);
+          }
+        }
+      }
+    }
+    amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
+    if (lane == 0) { red[0][sub] = amax; red[1][sub] = mn; red[2][sub] = mxo; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
+#pragma unroll
+    for (int w = 1; w < NSUB; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
+    unsigned* stt = p.mv.stat + 4 * slot;
+    atomicMax(&stt[0], a0);
+    atomicMin(&stt[1], a1);
+    atomicMax(&stt[2], a2);
+  }
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_f32p(
+    const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, const int* __restrict__ list_off, int slot,
+    int iter, float eps, int ncand) {
+  constexpr int STAGE = (128 + 64) * 32;   // floats per stage
+  __shared__ __attribute__((aligned(16))) float st0[STAGE];
+  __shared__ __attribute__((aligned(16))) float st1[STAGE];
+  __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float st3[NS > 3 ? STAGE : 4];
+  float* const stp[4] = {st0, st1, st2, st3};
+  __shared__ unsigned red[3][4];
+  const int t1 = list_off[blockIdx.x + 1];
+  for (int t = list_off[blockIdx.x]; t < t1; ++t) {
+    const GemmTile tl = tiles[t];
+    if (tl.bm == 128) f32_tile<128, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+    else if (tl.bm == 64) f32_tile<64, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+    else f32_tile<32, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+    __syncthreads();   // the stages and `red` are reused by the next tile
+  }
+}
+
+void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
+                      float eps, int ncand, hipStream_t s) {
+  if (nslots > 0)
+    hipLaunchKernelGGL(k_gemm_f32p<3>, dim3(nslots), dim3(256), 0, s, d, tiles, list_off, slot, iter, eps, ncand);
+}
+
 // One block per (problem, row): rows [0, Ip) of P (fp32, padded, zero pads) -> P2 / eP.
 // `which` 0: P of every split problem; 1: M (rows [0, ldm)) -> M2 / eM.
 __global__ __launch_bounds__(256) void k_split_rows(const ProbDesc* __restrict__ probs, int which) {

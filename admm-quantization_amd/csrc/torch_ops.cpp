@@ -52,13 +52,16 @@ at::Tensor workspace(size_t nbytes, const at::Tensor& like) {
 // --- admm_iteration_batched -------------------------------------------------------
 // solve: -1 = the process default (admmq_set_solve_mode; fp32 unless changed), else
 // ADMMQ_SOLVE_FP32 / ADMMQ_SOLVE_SPLIT for this call.
-// The call syncs once at its end to read the internal-fault column of `info`: when the
-// fused finalize's bounded wait timed out somewhere (its launch's blocks were not all
-// resident), the call restores U and re-runs with the separate finalize launch, so it
-// never returns unfinalized factors (same results as an undisturbed run).
+// check_fault (default): the call syncs once at its end to read the internal-fault column
+// of `info`: when the fused finalize's bounded wait timed out somewhere (its launch's
+// blocks were not all resident), the call restores U and re-runs with the separate
+// finalize launch, so it never returns unfinalized factors (same results as an
+// undisturbed run). check_fault = false: no sync; the caller must check info[:, 3]
+// itself and repeat the call (with U restored) where it is nonzero.
 std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> admm_batched_cuda(
     at::TensorList H, at::TensorList U, at::TensorList F, at::TensorList G, int64_t max_iter, double eps,
-    int64_t bits, int64_t qscheme, int64_t num_attempts, bool check_spd, bool debug, int64_t solve) {
+    int64_t bits, int64_t qscheme, int64_t num_attempts, bool check_spd, bool debug, int64_t solve,
+    bool check_fault) {
   const size_t n = H.size();
   TORCH_CHECK(n > 0, "admmq: admm_iteration_batched needs at least one problem");
   TORCH_CHECK(U.size() == n && F.size() == n && G.size() == n, "admmq: H, U, F, G lists differ in length");
@@ -114,7 +117,8 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
     return {same, info, hts, xs};
   }
   std::vector<at::Tensor> ubak;   // U before the run: restored if the run must be repeated
-  for (const at::Tensor& u : Uc) ubak.push_back(u.clone());
+  if (check_fault)
+    for (const at::Tensor& u : Uc) ubak.push_back(u.clone());
   auto run = [&]() {
     check_rc(admmq_admm_run_ex(probs.data(), nn, static_cast<int32_t>(max_iter), static_cast<float>(eps),
                                static_cast<int32_t>(bits), static_cast<int32_t>(qscheme), na, &opt, ws.data_ptr(),
@@ -122,7 +126,7 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
              "admm_run");
   };
   run();
-  if (info.select(1, 3).max().item<int32_t>() != 0) {   // internal fault: repeat without the fused finalize
+  if (check_fault && info.select(1, 3).max().item<int32_t>() != 0) {   // internal fault: repeat without the fused finalize
     for (size_t i = 0; i < n; ++i) Uc[i].copy_(ubak[i]);
     opt.fused_finalize = 0;
     check_rc(admmq_admm_prepare_ex(probs.data(), nn, na, &opt, ws.data_ptr(), ws.numel(), stream), "admm_prepare");
@@ -136,7 +140,8 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
 
 std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> admm_batched_meta(
     at::TensorList H, at::TensorList U, at::TensorList F, at::TensorList G, int64_t max_iter, double eps,
-    int64_t bits, int64_t qscheme, int64_t num_attempts, bool check_spd, bool debug, int64_t solve) {
+    int64_t bits, int64_t qscheme, int64_t num_attempts, bool check_spd, bool debug, int64_t solve,
+    bool check_fault) {
   std::vector<at::Tensor> outs, hts, xs;
   for (const at::Tensor& h : H) {
     outs.push_back(at::empty_like(h));
@@ -320,7 +325,7 @@ at::Tensor cp_rel_error_meta(at::TensorList W, at::TensorList factors) {
 
 TORCH_LIBRARY(admmq, m) {
   m.def("admm_iteration_batched(Tensor[] H, Tensor(a!)[] U, Tensor[] F, Tensor[] G, int max_iter, float eps, "
-        "int bits, int qscheme, int num_attempts=200, bool check_spd=True, bool debug=False, int solve=-1) "
+        "int bits, int qscheme, int num_attempts=200, bool check_spd=True, bool debug=False, int solve=-1, bool check_fault=True) "
         "-> (Tensor[] H_out, Tensor info, Tensor[] HT, Tensor[] X)");
   m.def("quantize_batched(Tensor[] x, int bits, int qscheme, int num_attempts=200, float? tmin=None, "
         "float? tmax=None) -> Tensor[]");

@@ -242,7 +242,7 @@ def step_roofline(work, max_iter_admm, ms_per_step, num_attempts=200):
             "split_solve_note": "solve term at the split form's f16 MFMA peak / 3 products (838.9 TF/s)"}
 
 
-TRAFFIC_TAG = "r02"
+TRAFFIC_TAG = "r03"
 
 
 def load_traffic(model, split):
@@ -324,6 +324,47 @@ def parity_check(device):
     return worst, exact
 
 
+def time_steps(work, max_iter_admm, steps, warmup):
+    for _ in range(warmup):
+        run_step(work, max_iter_admm)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run_step(work, max_iter_admm)
+    torch.cuda.synchronize()
+    return 1e3 * (time.perf_counter() - t0) / steps
+
+
+def emulate_shards(a):
+    """SURVEY §8(e) readiness without a node: every rank's LPT shard of an N-GPU
+    `--shard layers` run (bench.build_workload with that rank / world) is timed on this
+    one GPU with the same code path, plus the whole model; the implied N-GPU strong-scaling
+    speed-up is the whole model's ms per sweep over the busiest shard's (the final gather
+    of factors, ~20-400 MB over xGMI, is not included)."""
+    torch.cuda.set_device(0)
+    device = torch.device("cuda", 0)
+    from admmq import _lib
+    lib = _lib.load()
+    _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
+    N = a.emulate_world
+    full, _, _ = build_workload(a.model, 0, 1, "layers", device)
+    full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
+    del full
+    shard_ms, nlayers, info = [], [], None
+    for r in range(N):
+        work, _, info = build_workload(a.model, r, N, "layers", device)
+        nlayers.append(len(work))
+        shard_ms.append(time_steps(work, a.max_iter_admm, a.steps, a.warmup) if work else 0.0)
+        del work
+        print(f"shard {r}/{N}: {nlayers[-1]} layers, {shard_ms[-1]:.1f} ms per sweep", file=sys.stderr, flush=True)
+    out = {"metric": "emulated layer-shard sweep time (one GPU)", "model": a.model, "world": N, "solve": a.solve,
+           "max_iter_admm": a.max_iter_admm, "steps": a.steps, "full_ms_per_sweep": full_ms,
+           "shard_ms_per_sweep": shard_ms, "layers_per_rank": nlayers, "busiest_ms": max(shard_ms),
+           "implied_speedup": full_ms / max(shard_ms), "lpt_speedup_cap": info["lpt_speedup_cap"],
+           "whole_layer_speedup_cap": info["whole_layer_speedup_cap"], "policy": info["policy"]}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -339,13 +380,21 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP-event timing of one ADMM iteration in N (an event pair per launch adds a gap)")
-    ap.add_argument("--solve", choices=["split", "fp32"], default="split",
-                    help="per-iteration solve GEMM form: split-fp16 planes on f16 MFMA (default) or fp32 MFMA")
+    ap.add_argument("--solve", choices=["split", "fp32"], default="fp32",
+                    help="per-iteration solve GEMM form: fp32 MFMA (default: the reference's fp32 arithmetic) or "
+                         "split-fp16 planes on f16 MFMA (opt-in, ~22-bit operands; never the headline)")
     ap.add_argument("--exhaustive", action="store_true",
                     help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
     ap.add_argument("--search-units", type=int, default=0,
                     help="A/B: stage-1 units per block of the non-fused search launch (0: the planner's choice)")
+    ap.add_argument("--f32-tiles", type=int, default=-1,
+                    help="A/B: persistent fp32 solve tile rule 0..3 (-1: the library default; 9: the non-persistent k_gemm)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
+                         "(same code path, one after another) and report the busiest shard and the implied speed-up")
     a = ap.parse_args()
+    if a.emulate_world > 0:
+        return emulate_shards(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -360,6 +409,9 @@ def main():
     lib.admmq_set_exhaustive_search(1 if a.exhaustive else 0)
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
     _lib.check(lib.admmq_debug_set_search_units_per_block(a.search_units), "search_units_per_block")
+    if a.f32_tiles >= 0:
+        _lib.check(lib.admmq_debug_set_f32_persistent(0 if a.f32_tiles == 9 else 1, 0 if a.f32_tiles == 9 else a.f32_tiles),
+                   "f32_persistent")
     split = a.solve == "split"
     work, numel, shard_info = build_workload(a.model, rank, world, a.shard, device)
     fi_per_step = sum(len(s.shape) * (a.max_iter_admm - 1) for (s, _, _, _) in work)

@@ -189,3 +189,57 @@ def test_wide_tiles_equal_64x64(torch_dev):
             h1, u1 = run([small, big])
             h2, u2 = run([small])
         assert torch.equal(h1, h2) and torch.equal(u1, u2), form
+
+
+def _llama_layer_problems(torch, dev, mode, seed=7):
+    """Mode `mode` of all 7 matrices of one Llama-7B decoder layer, as bench.py's C5 step
+    batches them (notebooks/LlamaADMMQuant.ipynb cell 8 shapes; R = int(numel / sum(shape) / 2)):
+    q/k/v/o (4096, 4096) R=1024, gate/up (11008, 4096) R=1492, down (4096, 11008) R=1492.
+    Mode 0: F = W B, G = B^T B; mode 1: F = W^T A, G = A^T A (scripts/factorize.py:276-287)."""
+    shapes = [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)]
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for k, (I, J) in enumerate(shapes):
+        R = int(I * J / (I + J) / 2.0)
+        W = (torch.randn(I, J, generator=g) * 0.02).to(dev)
+        A = torch.randn(I, R, generator=g).to(dev)
+        B = torch.randn(J, R, generator=g).to(dev)
+        if mode == 0:
+            out.append((f"m{k}", A, W @ B, B.T @ B))
+        else:
+            out.append((f"m{k}", B, W.T @ A, A.T @ A))
+    return out
+
+
+@pytest.mark.parametrize("solve", ["fp32", "split"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_c5_llama_full_layer_batch(torch_dev, mode, solve):
+    """The whole C5 batched call bench.py times (7 matrices, wide tiles, non-fused search):
+    every problem's H_T within 1e-5 of an fp64 solve of the reference's formulation
+    (source/admm.py:53-57, on the device in fp64 as the checker), the projection
+    bit-exact (C oracle on the kernel's own X) and the dual update bit-exact. Covers the
+    (4096, R=1492) factors (down mode 0, gate/up mode 1) too."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    probs = _llama_layer_problems(torch, dev, mode)
+    rng = np.random.default_rng(21 + mode)
+    U0s = [torch.from_numpy((rng.standard_normal(tuple(H.shape)) * 1e-3).astype(np.float32)).to(dev)
+           for (_, H, _, _) in probs]
+    ps = [(H, U0.clone(), F, G) for (_, H, F, G), U0 in zip(probs, U0s)]
+    Hs, dbg = admm_iteration_batched(ps, 2, 1e-8, 4, MSE, debug_outputs=True, solve=solve)
+    worst = 0.0
+    for (name, H0, F, G), U0, H, (HT, X), p in zip(probs, U0s, Hs, dbg, ps):
+        R = G.shape[0]
+        rho = (torch.diagonal(G).sum() / R).double()     # fp32 sum, as source/admm.py:53
+        A64 = G.double() + rho * torch.eye(R, device=dev, dtype=torch.float64)
+        P64 = F.double() + rho * (H0.double() + U0.double())
+        ref = torch.cholesky_solve(P64.T, torch.linalg.cholesky(A64)).T
+        rel = float(torch.linalg.norm(HT.double() - ref) / torch.linalg.norm(ref))
+        worst = max(worst, rel)
+        assert rel < 1e-5, (name, rel)
+        X, H, U, HT, U0n = (t.cpu().numpy() for t in (X, H, p[1], HT, U0))
+        assert np.array_equal(_bits(X), _bits((HT - U0n).astype(np.float32))), name
+        Hq, _ = qc.quantize_mse(X, 4)
+        assert np.array_equal(_bits(H), _bits(Hq)), name
+        assert np.array_equal(_bits(U), _bits((U0n + (Hq - HT).astype(np.float32)).astype(np.float32))), name
+    print(f"C5 full layer mode {mode} {solve}: worst H_T rel vs fp64 {worst:.2e}")

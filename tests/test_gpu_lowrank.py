@@ -5,7 +5,8 @@ against the reference's outputs (tests/golden/f6_lowrank.npz) and the oracle.
     bit-exact quantizer, device break test);
   * rank side (rocSOLVER SVD vs torch-CPU LAPACK): 1e-4 rel-Frobenius (the fixture's
     random 96 x 64 start has close 4th/5th singular values; measured 1.3e-5 after 2 steps);
-  * SubspaceProjector vs exact truncation: 1e-4 rel-Frobenius;
+  * SubspaceProjector vs exact truncation: 1e-4 rel-Frobenius (decaying spectra);
+  * KrylovProjector vs exact float64 truncation: 1e-4 on the loop's own flat-spectrum iterates;
   * three outer iterations: rel errors within 1e-3 of the reference's.
 """
 import os
@@ -75,6 +76,42 @@ def test_subspace_projector_matches_svd(env):
         again = P(X * 1.0001)                       # warm start: converges in a few sweeps
         assert P.sweeps[-1] <= 6, P.sweeps
         assert _rel(again.cpu().numpy(), project_rank(X * 1.0001, r).cpu().numpy()) < 1e-4
+
+
+def test_krylov_projector_on_the_loops_flat_spectrum_iterate(env):
+    """The projection the (f)3 timing uses (KrylovProjector) on the low-rank ADMM's OWN
+    inputs at the notebook's shape (q_proj 4096 x 4096, synthetic N(0, 0.02^2), 4-bit
+    tensor_minmax, rank 8): their spectrum is flat (sigma_8 / sigma_9 ~ 1 + 1e-3), where a
+    subspace iteration stalls. Cold and warm-started, it must agree with the exact float64
+    SVD truncation to 1e-4 rel-Frobenius (scripts/factorize_lowrank.py:80-82)."""
+    torch, dev, _ = env
+    from functools import partial
+    from admmq import synthetic
+    from admmq.lowrank import KrylovProjector, admm_iteration
+    from admmq.quantization import quantize_tensor
+    W = torch.from_numpy(synthetic.layer_weight(synthetic.llama_layers()[0], 0)).to(dev)
+    g = torch.Generator().manual_seed(42)
+    quant = partial(quantize_tensor, qscheme="tensor_minmax", bits=4)
+    kry = KrylovProjector(8, seed=42)
+    seen = []
+
+    def proj(X):
+        seen.append(X.detach().clone())
+        return kry(X)
+    W_q, U_q = torch.randn(*W.shape, generator=g).to(dev), torch.zeros(W.shape, device=dev)
+    W_r = proj(torch.randn(*W.shape, generator=g).to(dev))
+    U_r = torch.zeros_like(W_r)
+    for _ in range(2):   # two outer iterations of the notebook loop, 4 inner steps each
+        W_q, U_q = admm_iteration(W_q, U_q, W, W_r, quant, rho=1.0, max_iter=5)
+        W_r, U_r = admm_iteration(W_r, U_r, W, W_q, proj, rho=1.0, max_iter=5)
+    for X in (seen[-1], seen[len(seen) // 2]):
+        Uu, S, Vt = torch.linalg.svd(X.double(), full_matrices=False)
+        exact = (Uu[:, :8] * S[:8]) @ Vt[:8]
+        gap = float(S[7] / S[8])
+        for P in (KrylovProjector(8, seed=3), kry):   # cold, and warm from the loop's state
+            rel = float(torch.linalg.norm(P(X).double() - exact) / torch.linalg.norm(exact))
+            print(f"sigma8/sigma9 {gap:.5f}: rel {rel:.2e}, blocks {P.blocks[-1]}")
+            assert rel < 1e-4, (gap, rel, P.blocks)
 
 
 @pytest.mark.parametrize("qs", ["tensor_minmax", "tensor_mseminmax_symmetric"])

@@ -14,7 +14,7 @@ from conftest import gpu_available
 SCHEMAS = {
     "admm_iteration_batched": "admmq::admm_iteration_batched(Tensor[] H, Tensor(a!)[] U, Tensor[] F, Tensor[] G, "
                               "int max_iter, float eps, int bits, int qscheme, int num_attempts=200, "
-                              "bool check_spd=True, bool debug=False, int solve=-1) -> (Tensor[] H_out, Tensor info, Tensor[] HT, "
+                              "bool check_spd=True, bool debug=False, int solve=-1, bool check_fault=True) -> (Tensor[] H_out, Tensor info, Tensor[] HT, "
                               "Tensor[] X)",
     "quantize_batched": "admmq::quantize_batched(Tensor[] x, int bits, int qscheme, int num_attempts=200, "
                         "float? tmin=None, float? tmax=None) -> Tensor[]",

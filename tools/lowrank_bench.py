@@ -7,12 +7,15 @@ the quantized part and for the low-rank part; 2 h 32 min 18 s wall on an A100,
 
 Runs, on one MI355X:
   * the full 100-outer-iteration loop with the device rank projection
-    (admmq.lowrank.SubspaceProjector: warm-started block subspace iteration on the
-    device, thin GEMMs + a 16 x 4096 SVD per sweep), wall-timed;
-  * the reference's exact projection (torch.linalg.svd of the 4096 x 4096 iterate, the
-    notebook's project_rank) timed on a bounded sample: SVD calls, then extrapolated
-    to the exact-projection loop's projection count;
-  * agreement of the two projections on the loop's final low-rank target W - W_q.
+    (admmq.lowrank.KrylovProjector: warm-started float64 block Krylov that stops at a
+    residual bound, so every projection agrees with the exact truncation), wall-timed;
+  * agreement of that projection with the exact truncation (float64 SVD) on sampled
+    inputs of the loop itself (its own flat-spectrum iterates), with their spectral gap;
+  * the reference's exact projection (torch.linalg.svd of the 4096 x 4096 float32
+    iterate, the notebook's project_rank) timed on a bounded sample and extrapolated to
+    the reference's schedule: up to 49 projections per admm_iteration(max_iter=50) call,
+    100 calls (the bound) and the loop's own count (its early exits; with projections
+    that agree with the exact ones the loop follows the exact loop's schedule).
 Prints one JSON line.  usage: tools/lowrank_bench.py [--outer 100] [--svd-sample 4]
 """
 import argparse
@@ -27,7 +30,7 @@ import torch  # noqa: E402
 from functools import partial  # noqa: E402
 
 from admmq import synthetic  # noqa: E402
-from admmq.lowrank import SubspaceProjector, admm_iteration, project_rank  # noqa: E402
+from admmq.lowrank import KrylovProjector, admm_iteration, project_rank  # noqa: E402
 from admmq.quantization import quantize_tensor  # noqa: E402
 
 A100_SECONDS = 2 * 3600 + 32 * 60 + 18
@@ -40,6 +43,8 @@ def main():
     ap.add_argument("--rank", type=int, default=8)
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--svd-sample", type=int, default=4, help="exact SVD projections timed (extrapolated)")
+    ap.add_argument("--check", type=str, default="0,1,48,500,2000,-1",
+                    help="projection calls whose input is checked against the exact float64 truncation (-1: last)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     spec = synthetic.llama_layers()[0]
@@ -57,10 +62,19 @@ def main():
     torch.cuda.synchronize()
     svd_s = (time.perf_counter() - t0) / a.svd_sample
 
-    # the notebook loop with the device projection
+    # the notebook loop with the device projection; inputs of some calls kept for the check
     W_q = torch.randn(*W.shape, generator=g).to(dev)
     U_q = torch.zeros_like(W_q)
-    proj = SubspaceProjector(a.rank, seed=42)
+    kry = KrylovProjector(a.rank, seed=42)
+    want = {int(c) for c in a.check.split(",")}
+    kept, calls = {}, [0]
+
+    def proj(X):
+        if calls[0] in want:
+            kept[calls[0]] = X.detach().clone()
+        kept["last"] = X
+        calls[0] += 1
+        return kry(X)
     W_r = proj(torch.randn(*W.shape, generator=g).to(dev))
     U_r = torch.zeros_like(W_r)
     torch.cuda.synchronize()
@@ -76,22 +90,36 @@ def main():
             print(f"outer {i}: rel {hist[-1]}", flush=True)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    # agreement of the device projection with the exact truncation on the loop's own
-    # low-rank target W - W_q (fresh projector, cold start) and that matrix's spectral gap
-    Xe = (W - W_q).contiguous()
-    exact = project_rank(Xe, a.rank)
-    approx = SubspaceProjector(a.rank, seed=1)(Xe)
-    agree = float(torch.linalg.norm(approx - exact) / torch.linalg.norm(exact))
-    sv = torch.linalg.svdvals(Xe)
-    gap = float(sv[a.rank - 1] / sv[a.rank])
+    # agreement with the exact truncation on the loop's own projection inputs: the exact
+    # float64 SVD truncation vs a fresh KrylovProjector (cold start: the harder case)
+    if -1 in want:
+        kept[calls[0] - 1] = kept["last"]
+    kept.pop("last", None)
+    checks = []
+    for c in sorted(kept):
+        X = kept[c]
+        Uu, S, Vt = torch.linalg.svd(X.double(), full_matrices=False)
+        exact = (Uu[:, :a.rank] * S[:a.rank]) @ Vt[:a.rank]
+        approx = KrylovProjector(a.rank, seed=1)(X).double()
+        ref32 = project_rank(X, a.rank).double()   # the reference's own float32 truncation
+        checks.append({"call": c, "rel_vs_exact_f64": float(torch.linalg.norm(approx - exact) / torch.linalg.norm(exact)),
+                       "reference_f32_svd_rel_vs_exact_f64": float(torch.linalg.norm(ref32 - exact) / torch.linalg.norm(exact)),
+                       "sigma_r_over_sigma_r1": float(S[a.rank - 1] / S[a.rank])})
+        print(checks[-1], flush=True)
+    sched_max = a.outer * (a.inner - 1)
     out = {"config": "LlamaADMMQuant.ipynb cell 15: q_proj 4096x4096 synthetic N(0,0.02^2), 4-bit tensor_minmax, "
                      f"rank {a.rank}, {a.outer} outer x admm_iteration(max_iter={a.inner}) x 2",
-           "device_projection": "SubspaceProjector (warm-started block subspace iteration, k = rank + 8)",
+           "device_projection": f"KrylovProjector (float64 block Krylov, block {kry.block}, residual tol {kry.tol}, "
+                                "warm-started)",
            "wall_s": wall, "a100_reference_wall_s": A100_SECONDS, "speedup_vs_a100_notebook": A100_SECONDS / wall,
-           "inner_iterations": {"quant": nq, "rank": nr}, "subspace_sweeps_mean": sum(proj.sweeps) / len(proj.sweeps),
-           "rel_history": hist, "exact_svd_projection_s": svd_s,
-           "exact_svd_loop_estimate_s": svd_s * nr, "device_vs_exact_projection_rel": agree,
-           "sigma_r_over_sigma_r1": gap}
+           "inner_iterations": {"quant": nq, "rank": nr}, "rank_projection_calls": calls[0],
+           "krylov_blocks_mean": sum(kry.blocks) / len(kry.blocks), "krylov_residual_max": max(kry.residuals),
+           "rel_history": hist, "reference_rel_history_real_weights": [32.1919, 1.0278, 1.0150, 1.0079],
+           "projection_checks": checks,
+           "max_rel_vs_exact_f64": max(c["rel_vs_exact_f64"] for c in checks),
+           "exact_svd_projection_s": svd_s,
+           "exact_svd_loop_estimate_s": {"reference_schedule_max": svd_s * sched_max, "this_loop_schedule": svd_s * nr,
+                                         "reference_schedule_max_projections": sched_max, "this_loop_projections": nr}}
     print(json.dumps(out), flush=True)
 
 

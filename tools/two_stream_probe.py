@@ -17,6 +17,10 @@ MSE = "tensor_mseminmax_symmetric"
 dev = torch.device("cuda:0")
 specs = synthetic.MODELS["resnet18"]()
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 201
+fused = (sys.argv[2] != "nofused") if len(sys.argv) > 2 else True
+from admmq import _lib  # noqa: E402
+_lib.load().admmq_debug_set_fused_finalize(1 if fused else 0)
+print(f"fused finalize: {fused}; fp32 solve: {_lib.load().admmq_get_solve_mode() == 0}", flush=True)
 for mode in range(3):
     layers = []
     for i, s in enumerate(specs):
@@ -30,14 +34,21 @@ for mode in range(3):
 
     def run(groups):
         streams = [torch.cuda.Stream() for _ in groups]
+        infos = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for st, grp in zip(streams, groups):
             with torch.cuda.stream(st):
-                admm_iteration_batched([(probs[i][0], torch.zeros_like(probs[i][1]), probs[i][2], probs[i][3])
-                                        for i in grp], iters, 0.0, 4, MSE, check_spd=False)
+                _, info = admm_iteration_batched([(probs[i][0], torch.zeros_like(probs[i][1]), probs[i][2], probs[i][3])
+                                                  for i in grp], iters, 0.0, 4, MSE, check_spd=False, return_info=True,
+                                                 check_fault=False)
+                infos.append(info)
         torch.cuda.synchronize()
-        return time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        faults = sum(int(i[:, 3].sum()) for i in infos)
+        if faults:
+            print(f"  ({faults} problems hit the fused-finalize timeout)", flush=True)
+        return dt
 
     for k in (1, 2, 3):
         loads = [0.0] * k

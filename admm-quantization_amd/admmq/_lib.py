@@ -105,6 +105,7 @@ def load() -> ctypes.CDLL:
         "admmq_admm_run_ex": (I32, [P, I32, I32, F32, I32, I32, I32, P, P, S, P, P]),
         "admmq_debug_set_fin_wait_polls": (I32, [ctypes.c_uint32]),
         "admmq_debug_set_f32_persistent": (I32, [I32, I32]),
+        "admmq_debug_set_gemm_ks": (I32, [I32]),
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),

@@ -187,6 +187,9 @@ void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int 
                       int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s);
+extern int g_gemm_ks_f32;
+void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
+                      hipStream_t s);
 void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
                       float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
@@ -196,6 +199,7 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
 size_t hist_lds_bytes(int ncand, int bits);
 size_t hist3_lds_bytes(int ncand, int bits);
 int copy_hist_trace(unsigned long long* host, int n);
+int copy_gemm_trace(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
 int copy_fin_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);

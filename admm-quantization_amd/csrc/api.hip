@@ -85,7 +85,9 @@ static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
 // tiles of the R = 1141 layers left gaps only coarse tiles could not fill); 2 = 64 x 64 for
 // ld >= 1024, 32 x 64 for the others; 3 = 128 x 64 for ld >= 1024, 64 x 64 for the others.
 static std::atomic<int> g_f32_rule{1};
-static std::atomic<bool> g_f32p{false};  // persistent fp32 solve (diagnostics: slower than k_gemm)
+// fp32 solve kernel: 0 = k_gemm (64 x 64 tiles), 1 = persistent tile lists (k_gemm_f32p,
+// slower: DESIGN §7), 2 = one tile per workgroup with per-problem tile rows (k_gemm_f32t)
+static std::atomic<int> g_f32_kernel{0};
 static int f32_tile_rows(int I, int ld) {
   if (I <= 32) return 32;
   const int rule = g_f32_rule.load();
@@ -279,9 +281,11 @@ struct AdmmPlan {
   int ntiles_wide = 0, ntiles_big = 0, ntiles_small = 0;   // 256x128, 64x64, 32x64 tiles (in that order)
   // persistent fp32 solve (k_gemm_f32p): tiles in list order, workgroup b's list [off[b], off[b+1])
   bool f32p = false;
+  bool f32t = false;   // one tile per workgroup, tile rows per problem (k_gemm_f32t)
   std::vector<int> list_off;
   int* d_list_off = nullptr;
   int nslots = 0;
+  int ntiles_f32t = 0;
   bool wide = false;                                       // I > 64 factors take 256x128 tiles (k_gemm<8, 1, 3, *, 2>)
   int fin_groups = 1;             // float4 groups per thread of the finalize units
   int hist_nv = 1;
@@ -312,7 +316,8 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
   const int rounds = (n + ncu - 1) / ncu;
   const int full = n - (rounds - 1) * ncu;   // CUs 0 .. full-1 take `rounds` tiles, the rest one fewer
   std::vector<GemmTile> sorted = tiles;
-  std::stable_sort(sorted.begin(), sorted.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
+  auto cost = [](const GemmTile& t) { return (long long)t.nk * ((t.bm > 0 ? t.bm : 64) / 32); };   // 32-row K-steps
+  std::stable_sort(sorted.begin(), sorted.end(), [&](const GemmTile& a, const GemmTile& b) { return cost(a) > cost(b); });
   std::vector<std::vector<GemmTile>> bins(ncu);
   std::vector<long long> load(ncu, 0);
   // Among the least-loaded CUs, prefer the XCD (CU b mod 8) that already holds tiles of
@@ -333,7 +338,7 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
       if (best < 0 || key < best_key) { best = b; best_key = key; }
     }
     bins[best].push_back(t);
-    load[best] += t.nk;
+    load[best] += cost(t);
     cx[best % kXcd] += 1;
     rx[best % kXcd] += 1;
   }
@@ -386,7 +391,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    const bool f32p_prob = !pl.split && g_f32p.load() && !(pl.wide && a.I > 64) && a.I > kThinRows;
+    const bool f32p_prob = !pl.split && g_f32_kernel.load() != 0 && !(pl.wide && a.I > 64) && a.I > kThinRows;
     d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? kWideRows : (f32p_prob ? std::max(64, f32_tile_rows(a.I, rup(a.R, 32))) : 64));
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
@@ -469,7 +474,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     }
   }
   // persistent fp32 solve: every non-thin, non-wide factor in per-workgroup lists
-  pl.f32p = !pl.split && g_f32p.load();
+  pl.f32p = !pl.split && g_f32_kernel.load() == 1;
+  pl.f32t = !pl.split && g_f32_kernel.load() == 2;
   pl.list_off.clear();
   pl.nslots = 0;
   if (pl.f32p) {
@@ -493,9 +499,25 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     }
     pl.tiles = ft;   // the wide tiles (if any) are inserted in front below
   }
+  if (pl.f32t) {
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if (d.I <= kThinRows || (pl.wide && d.I > 64)) continue;
+      const int bm = f32_tile_rows(d.I, d.ld);
+      const int TM = (d.I + bm - 1) / bm, TN = (d.ld + 63) / 64;
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = 0; tn < TN; ++tn) {
+          GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32);
+          t.bm = bm;
+          pl.tiles.push_back(t);
+        }
+    }
+    order_tiles_for_cus(pl.tiles, 256, 3);
+    pl.ntiles_f32t = (int)pl.tiles.size();
+  }
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
-    if (pl.f32p) break;
+    if (pl.f32p || pl.f32t) break;
     if (d.I <= kThinRows || d.Ip == 32 || (pl.wide && d.I > 64)) continue;   // thin / 32-row / wide: elsewhere
     const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
     for (int g0 = 0; g0 < TN; g0 += 8)
@@ -503,16 +525,16 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
         for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
           pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
   }
-  if (!pl.f32p) order_tiles_for_cus(pl.tiles, 256, 3);
+  if (!pl.f32p && !pl.f32t) order_tiles_for_cus(pl.tiles, 256, 3);
   std::vector<GemmTile> small;
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
-    if (pl.f32p) break;
+    if (pl.f32p || pl.f32t) break;
     if (d.I <= kThinRows || d.Ip != 32) continue;
     const int TN = (d.ld + 63) / 64;
     for (int tn = 0; tn < TN; ++tn) small.push_back(mk_tile(i, 0, tn, tn == 0 ? 1 : 0, d.ld / 32));
   }
-  pl.ntiles_big = pl.f32p ? 0 : (int)pl.tiles.size();   // f32p: the tiles after the wide ones are list-ordered
+  pl.ntiles_big = (pl.f32p || pl.f32t) ? 0 : (int)pl.tiles.size();   // f32p / f32t: their own launches
   pl.ntiles_small = (int)small.size();
   pl.ntiles_wide = (int)wide.size();
   pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
@@ -814,9 +836,16 @@ int32_t admmq_debug_set_fin_wait_polls(uint32_t polls) {
 
 // diagnostics (not in include/admmq.h): persistent fp32 solve on/off and its tile rule
 // (f32_tile_rows; changes the bits of the factors whose tile rows change between 64 and 32)
-int32_t admmq_debug_set_f32_persistent(int32_t enable, int32_t rule) {
+int32_t admmq_debug_set_gemm_ks(int32_t ks) {
+  if (ks != 1 && ks != 2) return fail(ADMMQ_ERR_ARG, "ks must be 1 or 2");
+  g_gemm_ks_f32 = ks;
+  return ADMMQ_OK;
+}
+
+int32_t admmq_debug_set_f32_persistent(int32_t kernel, int32_t rule) {
   if (rule < 0 || rule > 3) return fail(ADMMQ_ERR_ARG, "rule must be 0..3");
-  g_f32p = enable != 0;
+  if (kernel < 0 || kernel > 2) return fail(ADMMQ_ERR_ARG, "kernel must be 0..2");
+  g_f32_kernel = kernel;
   g_f32_rule = rule;
   return ADMMQ_OK;
 }
@@ -974,7 +1003,7 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
-    if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big + pl.nslots > 0) {
+    if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big + pl.nslots + pl.ntiles_f32t > 0) {
       prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
       if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0)
         launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
@@ -982,6 +1011,8 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
       if (pl.nslots > 0)
         launch_gemm_f32p(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.d_list_off, pl.nslots, slot, it, eps, num_attempts,
                          s);
+      if (pl.ntiles_f32t > 0)
+        launch_gemm_f32t(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.ntiles_f32t, slot, it, eps, num_attempts, s);
       prof_mark(s);
     }
     if (!pl.thin.empty()) {
@@ -1044,6 +1075,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 
 // diagnostics (not in include/admmq.h): per-block timelines of the last launches (make TRACE=1)
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
+int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
 int32_t admmq_debug_fin_trace(unsigned long long* host, int32_t n) { return copy_fin_trace(host, n); }
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }

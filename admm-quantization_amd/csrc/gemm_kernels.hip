@@ -38,6 +38,13 @@
 
 #include "quant_device.h"
 
+// Diagnostic builds only (EXTRA=-DADMMQ_GEMM_DIAG=n, never the product library; results
+// are garbage): 1 = the fp32 K-loop without its MFMAs (staging + fragment reads only),
+// 2 = without its global -> LDS staging after the first stages (fragment reads + MFMAs).
+#ifndef ADMMQ_GEMM_DIAG
+#define ADMMQ_GEMM_DIAG 0
+#endif
+
 namespace admmq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -90,13 +97,24 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16x8, v); }
 
+// Diagnostics (make TRACE=1 only): per workgroup of the last k_gemm launch {start, end,
+// (block << 48) | (K-steps << 40) | (XCC_ID << 32) | HW_ID} (admmq_debug_gemm_trace, tools/gemm_timeline.py)
+constexpr int kGemmTraceMax = 8192;
+__device__ unsigned long long g_gemm_trace[kGemmTraceMax][4];   // + shader-clock cycles of the workgroup
+int copy_gemm_trace(unsigned long long* host, int n) {
+  n = n < kGemmTraceMax ? n : kGemmTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
+
 // One workgroup per tile (the grid is the tile list, longest K first, CU-balanced by the
 // planner). SPLIT selects the operand form (see the file header).
 // CW: 32-column sub-tiles per wave (1: BN = 64 columns per tile; 2: 128, each wave's A
 // fragment feeding two sub-tiles - the wide tiles of large launches, CW = 2 with WM = 4:
 // 128 x 128, 8 waves, a third fewer operand bytes per MAC than 128 x 64).
 template <int WM, int KS, int NS, bool SPLIT, int CW = 1>
-__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(WM == 8 ? 4 : (NS <= 3 ? (WM == 4 ? 4 : 3) : 1)))) void k_gemm(
+__global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
+    WM == 8 ? 4 : (WM == 2 && KS == 2 ? 5 : (NS <= 3 ? (WM == 4 ? 4 : 3) : 1))))) void k_gemm(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 32 * WM;
   constexpr int BNT = BN * CW;                 // tile columns
@@ -133,6 +151,8 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
   const int swz = (i >> 1) & 7;
   const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * CW * wn + i) * 32;   // sub-tile c: boff + 32 * 32 c
 
+  const unsigned long long T0 = ADMMQ_NOW();
+  const unsigned long long C0 = ADMMQ_TRACE ? __builtin_amdgcn_s_memtime() : 0ull;
   const GemmTile tl = tiles[blockIdx.x];
   const ProbDesc& p = probs[tl.prob];
   const int ld = tl.ld, ldm = tl.ldm;
@@ -143,7 +163,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
   // loads complete in issue order: the stage waits below then also cover these)
   // (wide tiles, WM = 4: loaded in the epilogue instead - those launches run many rounds
   // of tiles, so other workgroups cover the latency, and the registers stay free)
-  constexpr bool PRE = WM < 4;   // (WM >= 4: the epilogue loads after the K-loop)
+  constexpr bool PRE = WM < 4 && !(WM == 2 && KS == 2);   // (WM >= 4 and the 8-wave 64 x 64 tiles: the epilogue loads after the K-loop)
   float upre[CW][16];
   int epre[16];
   int ecol[CW] = {};
@@ -217,7 +237,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
     wait_vmcnt<GPW * (NS - 2)>();                                                             \
     __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
     raw_barrier();                                                                            \
-    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
+    if (ADMMQ_GEMM_DIAG != 2 || SPLIT) ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1)); \
     const float* st = stp[s];                                                                 \
     if constexpr (SPLIT) {                                                                    \
       _Pragma("unroll") for (int q = 0; q < KCW; ++q) {                                       \
@@ -233,17 +253,35 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[c], 0, 0, 0);           \
         }                                                                                     \
       }                                                                                       \
-    } else {                                                                                  \
+    } else {   /* fragments of group qq + 1 read while group qq's MFMAs run (2 register sets) */ \
+      float4 fa[2], fb[2][CW];                                                                \
       _Pragma("unroll") for (int qq = 0; qq < QS; ++qq) {                                     \
-        const int cpos = ((4 * h + QS * ks + qq) ^ swz) * 4;                                  \
-        const float4 a = *reinterpret_cast<const float4*>(st + aoff + cpos);                  \
+        if (qq == 0) {                                                                        \
+          const int cp = ((4 * h + QS * ks) ^ swz) * 4;                                       \
+          fa[0] = *reinterpret_cast<const float4*>(st + aoff + cp);                           \
+          _Pragma("unroll") for (int c = 0; c < CW; ++c)                                      \
+            fb[0][c] = *reinterpret_cast<const float4*>(st + boff + 1024 * c + cp);           \
+          __builtin_amdgcn_sched_group_barrier(0x100, 1 + CW, 0);                             \
+        }                                                                                     \
+        if (qq + 1 < QS) {                                                                    \
+          const int cn = ((4 * h + QS * ks + qq + 1) ^ swz) * 4;                              \
+          fa[(qq + 1) & 1] = *reinterpret_cast<const float4*>(st + aoff + cn);                \
+          _Pragma("unroll") for (int c = 0; c < CW; ++c)                                      \
+            fb[(qq + 1) & 1][c] = *reinterpret_cast<const float4*>(st + boff + 1024 * c + cn); \
+          __builtin_amdgcn_sched_group_barrier(0x100, 1 + CW, 0);                             \
+        }                                                                                     \
         _Pragma("unroll") for (int c = 0; c < CW; ++c) {                                      \
-          const float4 b = *reinterpret_cast<const float4*>(st + boff + 1024 * c + cpos);     \
+          const float4 a = fa[qq & 1], b = fb[qq & 1][c];                                     \
+          if (ADMMQ_GEMM_DIAG == 1) {                                                         \
+            acc[c][0] += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;                       \
+          } else {                                                                            \
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[c], 0, 0, 0);           \
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[c], 0, 0, 0);           \
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[c], 0, 0, 0);           \
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[c], 0, 0, 0);           \
+          }                                                                                   \
         }                                                                                     \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * CW, 0);                               \
       }                                                                                       \
     }                                                                                         \
   } while (0)
@@ -317,6 +355,15 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(W
     atomicMax(&st[0], a0);
     atomicMin(&st[1], a1);
     atomicMax(&st[2], a2);
+    if (ADMMQ_TRACE && blockIdx.x < kGemmTraceMax) {
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+      g_gemm_trace[blockIdx.x][0] = T0;
+      g_gemm_trace[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - C0;
+      g_gemm_trace[blockIdx.x][1] = ADMMQ_NOW();
+      g_gemm_trace[blockIdx.x][2] = ((unsigned long long)blockIdx.x << 48) | ((unsigned long long)(nk & 0xFF) << 40) |
+                                    ((unsigned long long)(xcc & 0xFF) << 32) | hw;
+    }
   }
 }
 
@@ -356,18 +403,23 @@ __device__ __forceinline__ void f32_tile(const ProbDesc* __restrict__ probs, con
   const int ld = tl.ld, ldm = tl.ldm;
   const int row0 = tl.tm * BM, col0 = tl.tn * 64;
   const int nk = tl.nk;
-  // the epilogue's U entries, loaded first (their latency is spent under the K-loop)
+  // the epilogue's U entries: loaded first (their latency is spent under the K-loop),
+  // except for the two-accumulator waves (BM 128), which load them after the K-loop
+  constexpr bool PRE = CW == 1;
   float upre[CW][16];
+  auto load_u = [&]() {
 #pragma unroll
-  for (int c = 0; c < CW; ++c) {
-    const int col = col0 + 32 * (CW * wn + c) + i;
-    const int colc = col < ld ? col : 0;
+    for (int c = 0; c < CW; ++c) {
+      const int col = col0 + 32 * (CW * wn + c) + i;
+      const int colc = col < ld ? col : 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-      upre[c][r] = ldg(tl.U + (size_t)row * ld + colc);
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+        upre[c][r] = ldg(tl.U + (size_t)row * ld + colc);
+      }
     }
-  }
+  };
+  if constexpr (PRE) load_u();
   const float* src[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
@@ -456,6 +508,7 @@ __device__ __forceinline__ void f32_tile(const ProbDesc* __restrict__ probs, con
   }
   // epilogue (waves ks == 0): C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   if (ks == 0) {
+    if constexpr (!PRE) load_u();
     unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
     typedef __attribute__((address_space(1))) float gf32;
     gf32* const HTg = (gf32*)p.HT;
@@ -516,6 +569,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     else f32_tile<32, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
     __syncthreads();   // the stages and `red` are reused by the next tile
   }
+}
+
+// One fp32 tile per workgroup (k_gemm's grid form) with the persistent kernel's tile
+// shapes: BM 128 x 64 (4 waves of 32 x 64) for the large factors, 64 x 64 (2 x 2 waves)
+// for the others, in one launch; a 2-deep ring of (128 + 64)-row stages (48 KB: three
+// workgroups per CU, like k_gemm's 64 x 64 tiles). With three workgroups sharing a CU,
+// one K-step of a workgroup spans ~3 K-steps of MFMA time, longer than a load's latency,
+// so one stage in flight is enough.
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_gemm_f32t(
+    const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
+  constexpr int STAGE = (128 + 64) * 32;   // floats per stage
+  __shared__ __attribute__((aligned(16))) float st0[STAGE];
+  __shared__ __attribute__((aligned(16))) float st1[STAGE];
+  __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float st3[NS > 3 ? STAGE : 4];
+  float* const stp[4] = {st0, st1, st2, st3};
+  __shared__ unsigned red[3][4];
+  const GemmTile tl = tiles[blockIdx.x];
+  if (tl.bm == 128) f32_tile<128, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+  else if (tl.bm == 64) f32_tile<64, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+  else f32_tile<32, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
+}
+
+void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
+                      hipStream_t s) {
+  if (ntiles > 0)
+    hipLaunchKernelGGL(k_gemm_f32t<2>, dim3(ntiles), dim3(256), 0, s, d, tiles, slot, iter, eps, ncand);
 }
 
 void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
@@ -777,6 +858,10 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
   if (nprob > 0 && maxrows > 0) hipLaunchKernelGGL(k_split_rows, dim3(maxrows, nprob), dim3(256), 0, s, d, which);
 }
 
+// fp32 64 x 64 tiles: 1 = four waves of 32 x 32 (default), 2 = eight waves, each pair
+// splitting a sub-tile's K-step (two half chains summed in fixed order: other bits)
+int g_gemm_ks_f32 = 1;
+
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s) {
   // tiles[0 .. ntiles_wide) are 256x128 (WM = 8, CW = 2: sixteen waves of 32 x 64, the
@@ -796,7 +881,13 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
     else
       hipLaunchKernelGGL((k_gemm<8, 1, 3, false, 2>), dim3(ntiles_wide), dim3(1024), 0, s, d, tiles, slot, iter, eps, ncand);
   }
-  if (ntiles_big > 0) ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
+  if (ntiles_big > 0) {
+    if (!split && g_gemm_ks_f32 == 2)   // 8 waves per 64 x 64 tile, each K-step split over two waves (A/B)
+      hipLaunchKernelGGL((k_gemm<2, 2, 3, false>), dim3(ntiles_big), dim3(512), 0, s, d, tiles + ntiles_wide, slot, iter,
+                         eps, ncand);
+    else
+      ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
+  }
   if (ntiles_small > 0) ADMMQ_GEMM(1, 2, 4, ntiles_small, tiles + ntiles_wide + ntiles_big);
 #undef ADMMQ_GEMM
 }

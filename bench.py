@@ -387,8 +387,11 @@ def main():
                     help="A/B: evaluate all MSE candidates (reference-style) instead of the two-stage search")
     ap.add_argument("--search-units", type=int, default=0,
                     help="A/B: stage-1 units per block of the non-fused search launch (0: the planner's choice)")
-    ap.add_argument("--f32-tiles", type=int, default=-1,
-                    help="A/B: persistent fp32 solve tile rule 0..3 (-1: the library default; 9: the non-persistent k_gemm)")
+    ap.add_argument("--f32-kernel", type=int, default=-1,
+                    help="A/B: fp32 solve kernel 0 = k_gemm, 1 = persistent lists, 2 = one tile per workgroup with "
+                         "per-problem tile rows (-1: library default)")
+    ap.add_argument("--f32-tiles", type=int, default=3, help="A/B: tile-row rule 0..3 of --f32-kernel 1 / 2")
+    ap.add_argument("--gemm-ks", type=int, default=1, help="A/B: fp32 64x64 tiles with 4 (1) or 8 (2) waves")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
@@ -409,9 +412,9 @@ def main():
     lib.admmq_set_exhaustive_search(1 if a.exhaustive else 0)
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
     _lib.check(lib.admmq_debug_set_search_units_per_block(a.search_units), "search_units_per_block")
-    if a.f32_tiles >= 0:
-        _lib.check(lib.admmq_debug_set_f32_persistent(0 if a.f32_tiles == 9 else 1, 0 if a.f32_tiles == 9 else a.f32_tiles),
-                   "f32_persistent")
+    _lib.check(lib.admmq_debug_set_gemm_ks(a.gemm_ks), "gemm_ks")
+    if a.f32_kernel >= 0:
+        _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")
     split = a.solve == "split"
     work, numel, shard_info = build_workload(a.model, rank, world, a.shard, device)
     fi_per_step = sum(len(s.shape) * (a.max_iter_admm - 1) for (s, _, _, _) in work)

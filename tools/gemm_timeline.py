@@ -39,23 +39,29 @@ torch.cuda.synchronize()
 lib = _lib.load()
 lib.admmq_debug_gemm_trace.restype = ctypes.c_int32
 n = 8192
-buf = (ctypes.c_ulonglong * (3 * n))()
+buf = (ctypes.c_ulonglong * (4 * n))()
 got = lib.admmq_debug_gemm_trace(buf, n)
 recs = []
+clk = []
 for b in range(got):
-    t0, t1, hid = buf[3 * b], buf[3 * b + 1], buf[3 * b + 2]
+    t0, t1, hid = buf[4 * b], buf[4 * b + 1], buf[4 * b + 2]
+    if t1 > t0:
+        clk.append(buf[4 * b + 3] / ((t1 - t0) / 100.0) / 1e3)   # shader cycles per us -> GHz
     if t0 == 0 or t1 < t0:
         break
     wg = hid >> 48
-    xcc = (hid >> 32) & 0xFFFF
+    nk = (hid >> 40) & 0xFF
+    xcc = (hid >> 32) & 0xFF
     hw = hid & 0xFFFFFFFF
     cu = (hw >> 8) & 0xF
     sh = (hw >> 12) & 1
     se = (hw >> 13) & 0x7
-    recs.append((b, t0, t1, xcc, se, sh, cu, wg))
+    recs.append((b, t0, t1, xcc, se, sh, cu, wg, nk))
 t0 = min(r[1] for r in recs)
 t1 = max(r[2] for r in recs)
 print(f"tiles {len(recs)}  span {(t1 - t0) / 100:.2f} us (100 MHz ticks)")
+clk.sort()
+print(f"in-kernel shader clock (s_memtime / s_memrealtime) GHz: min {clk[0]:.3f} median {clk[len(clk) // 2]:.3f} max {clk[-1]:.3f}")
 dur = [(r[2] - r[1]) / 100 for r in recs]
 print(f"tile duration us: min {min(dur):.2f} avg {sum(dur)/len(dur):.2f} max {max(dur):.2f}")
 print("first 8 tiles dur:", [round(x, 1) for x in dur[:8]], " last 8:", [round(x, 1) for x in dur[-8:]])
@@ -78,3 +84,29 @@ pairs = [(b, b + 256) for b in range(len(recs)) if b + 256 in where and b in whe
 same = sum(1 for a, b in pairs if where[a] == where[b])
 print(f"placement: workgroups b and b+256 on the same CU for {same}/{len(pairs)} pairs; "
       f"same XCD for {sum(1 for a, b in pairs if where[a][0] == where[b][0])}/{len(pairs)}")
+
+# per-CU view: K-steps carried, first start, last end (the launch is as long as the last CU)
+cus = collections.defaultdict(list)
+for r in recs:
+    cus[(r[3], r[4], r[5], r[6])].append(r)
+rows = []
+for k, v in cus.items():
+    ks = sum(x[8] for x in v)
+    rows.append(((max(x[2] for x in v) - t0) / 100, (min(x[1] for x in v) - t0) / 100, ks, len(v)))
+rows.sort()
+import statistics
+print(f"CUs {len(rows)}; K-steps per CU: max {max(r[2] for r in rows)} mean {statistics.mean(r[2] for r in rows):.1f}")
+print("CU end times (us) percentiles 0/10/50/90/100:",
+      [round(rows[int(q * (len(rows) - 1))][0], 1) for q in (0, 0.1, 0.5, 0.9, 1.0)])
+print("CU first-start (us) max:", round(max(r[1] for r in rows), 2))
+# us per K-step of a CU = end / K-steps (all tiles of a CU start at ~0)
+rate = sorted(r[0] / r[2] for r in rows if r[2])
+print("us per K-step per CU (64x64x32 units) percentiles 0/50/100:", [round(rate[int(q * (len(rate) - 1))], 3) for q in (0, .5, 1)])
+by_load = collections.defaultdict(list)
+for r in rows:
+    by_load[r[2]].append(r[0])
+print("end time by CU load (K-steps: mean end us, n):", {k: (round(statistics.mean(v), 1), len(v)) for k, v in sorted(by_load.items())})
+tile_rate = collections.defaultdict(list)
+for r in recs:
+    tile_rate[r[8]].append((r[2] - r[1]) / 100)
+print("tile duration by K-steps (mean us, n):", {k: (round(statistics.mean(v), 1), len(v)) for k, v in sorted(tile_rate.items())})

@@ -15,4 +15,5 @@ bash tools/profile.sh r03a resnet18 > gpurun_out/c_profile.log 2>&1 || exit $?
 timeout -k 10 300 python -u tools/two_stream_probe.py 201 fused > gpurun_out/c_2s_fused.log 2>&1 || exit $?
 timeout -k 10 300 python -u tools/two_stream_probe.py 201 nofused > gpurun_out/c_2s_nofused.log 2>&1 || exit $?
 timeout -k 10 900 python -u tools/lowrank_bench.py > gpurun_out/c_lowrank.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --gemm-ks 2 > gpurun_out/c_r18_ks2.log 2>&1 || exit $?
 echo done

@@ -106,6 +106,8 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_fin_wait_polls": (I32, [ctypes.c_uint32]),
         "admmq_debug_set_f32_persistent": (I32, [I32, I32]),
         "admmq_debug_set_gemm_ks": (I32, [I32]),
+        "admmq_debug_set_fin_capacity": (I32, [I32]),
+        "admmq_debug_set_thin_loop": (I32, [I32]),
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
         "admmq_mse_sse_table": (I32, [P, I64, I64, I32, I32, P, P, S, P]),
@@ -249,6 +251,39 @@ class fin_wait_polls:
 
     def __exit__(self, *exc):
         load().admmq_debug_set_fin_wait_polls(0)
+        return False
+
+
+class fin_capacity:
+    """Context manager (diagnostics): resident-block budget of the fused finalize (0: the
+    device's). A small budget forces its several-units-per-block form."""
+
+    def __init__(self, blocks: int):
+        self.blocks = blocks
+
+    def __enter__(self):
+        check(load().admmq_debug_set_fin_capacity(int(self.blocks)), "fin_capacity")
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_fin_capacity(0)
+        return False
+
+
+class thin_loop:
+    """Context manager: the persistent loop of the thin factors (k_thin_loop: every
+    iteration of a call whose factors all have I <= 16 in one launch; default on) or the
+    per-iteration launches. Restores the default on exit."""
+
+    def __init__(self, enable: bool):
+        self.enable = enable
+
+    def __enter__(self):
+        check(load().admmq_debug_set_thin_loop(1 if self.enable else 0), "thin_loop")
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_thin_loop(1)
         return False
 
 

@@ -35,9 +35,7 @@ constexpr int kHistRep = 8;        // replicas of the global stage-1 histograms 
 constexpr int kMaxMerged = 4096;   // qmax * ncand of the merged-threshold stage 1
 constexpr int kCells = 4096;       // coarse cells of the merged-threshold stage 1 (mse_search.hip)
 constexpr int kResRep = 8;         // replicas of the per-problem residual sums (atomic spread)
-constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU split-K solve
-constexpr int kThinCols = 256;     // ... columns per unit (64 lanes x float4)
-constexpr int kThinK = 128;        // ... reduction rows per unit (4 waves x 32)
+constexpr int kThinRows = 16;      // factors with I <= kThinRows take the VALU solve of thin_loop.hip
 constexpr long long kWideMinTiles = 4 * 768;   // 64x64 tiles of a launch from which I > 64 factors take wide tiles
 constexpr int kWideRows = 256;                 // ... of kWideRows x 128 (k_gemm<8, 1, 3, *, 2>)
 
@@ -83,8 +81,6 @@ struct ProbDesc {
   _Float16* M2; int* eM;    // [ldm] rows
   MseView mv;
   double* res;
-  float* Part;     // thin factors (I <= kThinRows): split-K partial sums [nkg][NR][ld]
-  unsigned* tcnt;  // thin factors: arrival counter per 256-column block
   int* flags;
   float* rho;
   int I, R, ld, Ip, ldm, nbk;
@@ -116,8 +112,28 @@ struct GemmTile {
   const int* eP; const int* eM;
   int ld, ldm;
 };
-// Thin-factor solve unit: 256 columns x 128 rows of the reduction of one problem
-struct ThinUnit { int prob, cb, kg, nkg, first, pad_[3]; };
+// Thin-factor solve workgroup (thin_loop.hip): columns [col0, col0 + cw) of problem `job`,
+// the rank-th of the problem's nteam workgroups (in the persistent loop rank 0 resets the
+// team's words)
+struct ThinLoopUnit { int job, col0, cw, rank, nteam, pad_[3]; };
+constexpr int kTLThreads = 512;
+constexpr int kTLMaxCand = 256;       // num_attempts of the persistent loop
+constexpr int kTLBins = 264;          // >= kTLMaxCand + 1, a whole number of 64-B lines
+constexpr int kTLKPairs = 9;          // k pairs of M per thread and reduction chunk (ld <= 1152 per chunk)
+// A team's hand-off words, one set per parity slot (zeroed by the host before the launch;
+// after that rank 0 re-zeroes a slot once every reader is past it). 128-B lines apart.
+struct alignas(128) ThinSync {
+  unsigned bar;                          // barrier arrivals (monotonic)
+  unsigned pad0_[31];
+  unsigned long long mx[2];              // max |X| bits per slot
+  unsigned long long pad1_[14];
+  double s2[2];                          // sum X^2 per slot (stage-1 bound)
+  double res[2][4];                      // residual sums S1..S4 per slot
+  double pad2_[6];
+  unsigned long long h1[2][kTLBins];     // stage-1 level sums (team total)
+  unsigned long long h2[2][kTLBins];
+  unsigned long long sse[2][kTLBins];    // stage-2 canonical SSE of the selected candidates
+};
 // Work unit {job, first element}. Stage-1 units also carry the job's inputs that the
 // kernel's first loads need (the search state, the stop flag, the tensor and its size),
 // so those loads do not wait on a dependent descriptor read.
@@ -183,8 +199,8 @@ void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
 void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
-void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
-                      int ncand, hipStream_t s);
+void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits, int nr, int maxld, int slot, int iter,
+                       float eps, int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s);
 extern int g_gemm_ks_f32;
@@ -193,6 +209,9 @@ void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int 
 void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
                       float eps, int ncand, hipStream_t s);
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s);
+// persistent thin-factor loop: 0 if launched, else why not (-1 unsupported shape, -2 no residency)
+int launch_thin_loop(const ProbDesc* d, const ThinLoopUnit* units, int nunits, ThinSync* sync, int nr, int maxld,
+                     int n_iter, float eps, int ncand, int bits, unsigned wait_polls, int ncu, hipStream_t s);
 // two-stage MSE search over MseView tables (ADMM: views embedded in ProbDesc)
 void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits,
                      int slot, int nv, hipStream_t s);

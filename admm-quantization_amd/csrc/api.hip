@@ -76,6 +76,12 @@ static std::atomic<int> g_hist_reps{0};
 // polls of the fused finalize's bounded wait for its job's selection (diagnostics can
 // shrink it to force the timeout path)
 static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
+// diagnostics: a smaller resident-block budget for the fused finalize (0: the device's),
+// to exercise its several-units-per-block form on small batches
+static std::atomic<int> g_fin_cap_override{0};
+// persistent loop of the thin factors (k_thin_loop) for calls whose problems are all
+// thin; off: the per-iteration launches (A/B and cross-check)
+static std::atomic<bool> g_thin_loop{true};
 
 // Tile rows of the persistent fp32 solve per problem (fixed by the problem's shape, never
 // by the batch, so every element's result is batch-independent): 0 = 64 x 64 tiles
@@ -263,6 +269,7 @@ struct AdmmPlan {
   std::vector<Chunk> sse_chunks, fin_chunks, hist_chunks;
   std::vector<Chunk> hist_multi;   // the same units, several per block (launches without the fused finalize)
   Chunk* d_hist_multi = nullptr;
+  Chunk* d_hist_fin = nullptr;     // fused finalize with several units per block (built in run)
   int nhm_big = 0;                 // hist_multi blocks of the big jobs (listed first)
   ProbDesc* d_desc = nullptr;
   GemmTile* d_tiles = nullptr;
@@ -270,10 +277,9 @@ struct AdmmPlan {
   Chunk* d_fin = nullptr;
   Chunk* d_hist = nullptr;
   bool split = false;            // per-iteration solve on the split fp16 planes (kSolveSplit)
-  std::vector<ThinUnit> thin;    // VALU split-K solve units of the thin (I <= kThinRows) factors
-  ThinUnit* d_thin = nullptr;
-  unsigned* d_tcnt = nullptr;    // their per-column-block arrival counters
-  int thin_nr = 0, ntcnt = 0;
+  std::vector<ThinLoopUnit> thin;   // solve workgroups (32 columns each) of the thin (I <= kThinRows) factors
+  ThinLoopUnit* d_thin = nullptr;
+  int thin_nr = 0, thin_maxld = 0;
   unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged), then the cell index (kCells + 2)
   unsigned short* d_groups = nullptr;   // merged stage-1 tie groups (3 kMaxMerged)
   size_t bytes = 0;
@@ -295,6 +301,10 @@ struct AdmmPlan {
   bool rows_aligned = true;          // every big job's stage-1 units are whole rows (fused finalize possible)
   unsigned* d_ready = nullptr;       // [nprob][2] fused-finalize ready words (zeroed per run)
   int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
+  // persistent thin-factor loop (k_thin_loop, one team of `thin` workgroups per problem):
+  // possible when every problem is thin, ld <= 1152 and the workgroups fit the CUs
+  ThinSync* d_tl_sync = nullptr;
+  bool tl_ok = false;
 };
 
 static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
@@ -414,8 +424,6 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       d.eM = cv.take<int>(d.ldm);
     }
     d.res = cv.take<double>(2 * kResRep * 4);
-    d.Part = thin ? cv.take<float>((size_t)((d.ld + kThinK - 1) / kThinK) * pl.thin_nr * d.ld) : nullptr;
-    d.tcnt = nullptr;
     d.flags = cv.take<int>(4);
     d.rho = cv.take<float>(4);
     carve_view(cv, d.mv, 2, ncand);
@@ -539,18 +547,20 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.ntiles_wide = (int)wide.size();
   pl.tiles.insert(pl.tiles.end(), small.begin(), small.end());
   pl.tiles.insert(pl.tiles.begin(), wide.begin(), wide.end());
-  // thin units, most reduction blocks first; counters: one per (problem, column block)
+  // thin factors: one solve workgroup per 32 columns (thin_loop.hip), longest rows first;
+  // the same list is the persistent loop's teams (rank = column block)
   pl.thin.clear();
-  pl.ntcnt = 0;
-  std::vector<int> tcnt_off(nprob, -1);
+  pl.thin_maxld = 0;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     if (d.I > kThinRows) continue;
-    const int nkg = (d.ld + kThinK - 1) / kThinK, ncb = (d.ld + kThinCols - 1) / kThinCols;
-    tcnt_off[i] = pl.ntcnt;
-    pl.ntcnt += ncb;
-    for (int kg = 0; kg < nkg; ++kg)
-      for (int cb = 0; cb < ncb; ++cb) pl.thin.push_back({i, cb, kg, nkg, (cb == 0 && kg == 0) ? 1 : 0, {0, 0, 0}});
+    pl.thin_maxld = std::max(pl.thin_maxld, d.ld);
+    for (int c = 0; c < d.ld; c += 32) {
+      ThinLoopUnit u;
+      std::memset(&u, 0, sizeof(u));
+      u.job = i; u.col0 = c; u.cw = 32; u.rank = c / 32; u.nteam = d.ld / 32;
+      pl.thin.push_back(u);
+    }
   }
   pl.sse_chunks.clear();
   pl.fin_chunks.clear();
@@ -633,11 +643,13 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_hist_multi = cv.take<Chunk>(pl.hist_multi.size());
+  pl.d_hist_fin = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
-  pl.d_thin = cv.take<ThinUnit>(pl.thin.size());
-  pl.d_tcnt = cv.take<unsigned>(std::max(pl.ntcnt, 1));
-  for (int i = 0; i < nprob; ++i)
-    if (tcnt_off[i] >= 0 && pl.d_tcnt) pl.desc[i].tcnt = pl.d_tcnt + tcnt_off[i];
+  pl.d_thin = cv.take<ThinLoopUnit>(pl.thin.size());
+  if ((int)pl.small.size() == nprob) {   // sized by the problems alone (not by the device's CUs)
+    pl.d_tl_sync = cv.take<ThinSync>(nprob);
+    pl.tl_ok = pl.thin_maxld <= 1152 && (int)pl.thin.size() <= device_cus();
+  }
   pl.d_rank0 = cv.take<unsigned short>(kMaxMerged + kCells + 2);
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
@@ -664,7 +676,7 @@ static int upload_admm(AdmmPlan& pl, hipStream_t s) {
   if ((rc = h2d(pl.d_fin, pl.fin_chunks.data(), pl.fin_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist_multi, pl.hist_multi.data(), pl.hist_multi.size() * sizeof(Chunk), s))) return rc;
-  if (!pl.thin.empty() && (rc = h2d(pl.d_thin, pl.thin.data(), pl.thin.size() * sizeof(ThinUnit), s))) return rc;
+  if (!pl.thin.empty() && (rc = h2d(pl.d_thin, pl.thin.data(), pl.thin.size() * sizeof(ThinLoopUnit), s))) return rc;
   if (!pl.small.empty() && (rc = h2d(pl.d_small, pl.small.data(), pl.small.size() * sizeof(int), s))) return rc;
   return check_hip("upload");
 }
@@ -827,6 +839,19 @@ size_t admmq_debug_admm_plan_bytes(const admmq_problem* probs, int32_t nprob, in
   return pl.bytes;
 }
 
+// diagnostics (not in include/admmq.h): resident-block budget of the fused finalize (0: the device's)
+int32_t admmq_debug_set_fin_capacity(int32_t blocks) {
+  if (blocks < 0) return fail(ADMMQ_ERR_ARG, "blocks must be >= 0");
+  g_fin_cap_override = blocks;
+  return ADMMQ_OK;
+}
+
+// diagnostics (not in include/admmq.h): the persistent thin-factor loop on / off
+int32_t admmq_debug_set_thin_loop(int32_t on) {
+  g_thin_loop = on != 0;
+  return ADMMQ_OK;
+}
+
 // diagnostics (not in include/admmq.h): polls of the fused finalize's bounded wait
 // (default kFinWaitPollsDefault; a test sets 1 to force the timeout / internal-fault path)
 int32_t admmq_debug_set_fin_wait_polls(uint32_t polls) {
@@ -976,8 +1001,6 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   hipStream_t s = static_cast<hipStream_t>(stream);
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
-  if (pl.ntcnt && hipMemsetAsync(pl.d_tcnt, 0, pl.ntcnt * sizeof(unsigned), s) != hipSuccess)
-    return check_hip("thin counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
@@ -994,12 +1017,60 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   // the big jobs' finalize inside the search launch when all its blocks fit at once
   // (with a margin of one resident block per CU: see hist3_fin_capacity)
   const int nh_big = fuse_small ? pl.nhist_big : nhist;
-  const bool fuse_fin = opt->fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned &&
-                        nh_big > 0 && nh_big <= hist3_fin_capacity(num_attempts, bits, pl.hist_nv);
+  const bool fin_ok = opt->fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0;
+  const int cap_over = g_fin_cap_override.load();
+  const int fin_cap = fin_ok ? (cap_over > 0 ? std::min(cap_over, hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
+                                             : hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
+                             : 0;
+  // more units than resident blocks: each block takes `fin_reps` consecutive units of its job
+  // (one table setup, flush and wait for all of them; their finalize re-reads the elements)
+  int fin_reps = 1, nfin_blocks = nh_big;
+  std::vector<Chunk> fin_multi;
+  // (measured at C4: no faster than the separate finalize launch, 324 vs 318 ms per sweep -
+  // the per-block serialization of reps units outweighs the saved launch; so only when a
+  // diagnostic budget asks for it)
+  if (fin_ok && fin_cap > 0 && nh_big > fin_cap && cap_over > 0) {
+    for (fin_reps = 2; fin_reps <= kHistMultiMaxReps; ++fin_reps) {
+      fin_multi.clear();
+      for (int a = 0; a < nh_big;) {
+        int b = a;
+        while (b < nh_big && pl.hist_chunks[b].job == pl.hist_chunks[a].job) ++b;
+        const int nblk = (b - a + fin_reps - 1) / fin_reps;
+        for (int c = a; c < b; c += fin_reps) {
+          const int e = std::min(b, c + fin_reps) - 1;
+          Chunk k = pl.hist_chunks[c];
+          k.reps = e - c + 1;
+          k.step = (int)(pl.hist_chunks[c].total - pl.hist_chunks[c].start);
+          k.total = pl.hist_chunks[e].total;
+          k.nblk = nblk;
+          fin_multi.push_back(k);
+        }
+        a = b;
+      }
+      if ((int)fin_multi.size() <= fin_cap) break;
+    }
+    nfin_blocks = (int)fin_multi.size();
+  }
+  const bool fuse_fin = fin_ok && fin_cap > 0 && nfin_blocks <= fin_cap;
+  if (fuse_fin && fin_reps > 1 && (rc = h2d(pl.d_hist_fin, fin_multi.data(), fin_multi.size() * sizeof(Chunk), s)))
+    return rc;
   const unsigned polls = g_fin_wait_polls.load();
   if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned), s) != hipSuccess)
     return check_hip("ready reset");
-  for (int it = 0; it + 1 < max_iter; ++it) {
+  // every problem thin: all iterations in one persistent launch (k_thin_loop) when the
+  // fused paths are allowed (the op's fault retry turns them off) and it fits the device
+  bool loop_done = false;
+  if (pl.tl_ok && g_thin_loop.load() && opt->fused_finalize && qscheme == kMse && !exhaustive && max_iter > 1 &&
+      num_attempts >= 2 && num_attempts <= kTLMaxCand && bits >= 2 && bits <= 5) {
+    if (hipMemsetAsync(pl.d_tl_sync, 0, (size_t)nprob * sizeof(ThinSync), s) != hipSuccess)
+      return check_hip("thin loop reset");
+    g_prof.sampled = true;
+    prof_class(ADMMQ_PROF_THIN_LOOP); prof_mark(s);
+    loop_done = launch_thin_loop(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.d_tl_sync, pl.thin_nr, pl.thin_maxld,
+                                 max_iter - 1, eps, num_attempts, bits, polls, device_cus(), s) == 0;
+    prof_mark(s);
+  }
+  for (int it = 0; !loop_done && it + 1 < max_iter; ++it) {
     const int slot = it & 1;
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
@@ -1017,19 +1088,20 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
     }
     if (!pl.thin.empty()) {
       prof_class(ADMMQ_PROF_GEMM_THIN); prof_mark(s);
-      launch_gemm_thin(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, slot, it, eps, num_attempts, s);
+      launch_thin_solve(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.thin_nr, pl.thin_maxld, slot, it, eps,
+                        num_attempts, s);
       prof_mark(s);
     }
     if (qscheme == kMse) {
       // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
         // fused finalize: one whole-row unit per block; otherwise several units per block
-        const int nh = fuse_fin ? (fuse_small ? pl.nhist_big : nhist)
-                                : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
+        const int nh = fuse_fin ? nfin_blocks : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
         if (nh > 0) {
           prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
-          launch_mse_hist3(pl.d_desc, nullptr, fuse_fin ? pl.d_hist : pl.d_hist_multi, nh, num_attempts, bits, slot,
-                           pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s);
+          launch_mse_hist3(pl.d_desc, nullptr,
+                           fuse_fin ? (fin_reps > 1 ? pl.d_hist_fin : pl.d_hist) : pl.d_hist_multi, nh, num_attempts,
+                           bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s);
           prof_mark(s);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each

@@ -631,229 +631,6 @@ __global__ __launch_bounds__(256) void k_split_rows(const ProbDesc* __restrict__
   if (threadIdx.x == 0) (which ? p.eM : p.eP)[row] = e;
 }
 
-// ---------------------------------------------------------------------------
-// Thin factors (I <= kThinRows, e.g. the 9-row spatial mode of a 3x3 conv): the solve
-// HT[I x ld] = P . M streams M once with only I useful rows per M element, so it is
-// an HBM/MALL stream, not an MFMA problem (a 32-row MFMA tile would waste 23/32 of the
-// matrix core and a whole-K tile per workgroup leaves most CUs idle). VALU split-K:
-// a unit is kThinCols columns x kThinK reduction rows of one problem; lane l owns
-// columns 4l..4l+3 of the block (one float4 of an M row per k), wave w the 32 rows
-// k0 + 32w.., all 32 float4 loads issued up front; P[0..NR)[k] come from LDS
-// (broadcast reads). The four wave partials are summed in LDS in wave order; with
-// nkg > 1 reduction blocks the block sum goes to Part (agent-scope stores, which
-// write through the XCD L2), the last block to arrive (per-column-block counter)
-// sums the nkg partials in kg order and runs the epilogue. Every sum is in a fixed
-// order: the result does not depend on which block arrives last.
-template <int NR>
-__global__ __launch_bounds__(256) void k_gemm_thin(const ProbDesc* __restrict__ probs,
-                                                   const ThinUnit* __restrict__ units, int slot, int iter,
-                                                   float eps, int ncand) {
-  constexpr int PS = (NR + 3) / 4 * 4;       // LDS row stride of the P transpose (b128 reads)
-  constexpr int RW = (NR + 3) / 4;           // epilogue rows per wave (rows w, w + 4, ...)
-  constexpr int PJ = (NR + 1) / 2;           // P loads per thread (rows t / 128 + 2 j)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  __shared__ __attribute__((aligned(16))) float Pt[kThinK][PS];
-  __shared__ __attribute__((aligned(16))) float red[4][NR][kThinCols];
-  __shared__ int s_last;
-  const ThinUnit u = units[blockIdx.x];
-  const ProbDesc& p = probs[u.prob];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ld = p.ld, ldm = p.ldm, I = p.I;
-  const int col = u.cb * kThinCols + 4 * lane;
-  const int kb = u.kg * kThinK;
-  const int k0 = kb + 32 * wave;
-  const bool cok = col < ld;
-  const int cc = min(col, ld - 4);
-  // Every load is issued before anything waits: P[0..NR)[kb .. kb + kThinK) (thread t:
-  // k = t % 128 of rows t / 128 + 2 j; rows >= I and k >= ld read as 0, the address is
-  // clamped so the loads are unconditional), the stop-test inputs, the U rows of the
-  // epilogue, then the M rows; the in-order vmcnt lets the first ones be used while the
-  // M rows are in flight.
-  const int pk = tid & (kThinK - 1), pi0 = tid >> 7;
-  const int pkc = min(kb + pk, ld - 1);
-  float pv[PJ];
-#pragma unroll
-  for (int j = 0; j < PJ; ++j) pv[j] = ldg(p.P + (size_t)(pi0 + 2 * j) * ld + pkc);   // rows < 16 <= Ip
-  const int done = *(__attribute__((address_space(1))) const int*)p.flags;
-  // residual replicas of the previous iteration: lane l < 32 holds entry l of [kResRep][4]
-  const double rv = (iter > 0 && lane < 4 * kResRep)
-                        ? *(__attribute__((address_space(1))) const double*)(p.res + 4 * kResRep * (slot ^ 1) + lane)
-                        : 0.0;
-  float4 uu[RW];
-#pragma unroll
-  for (int r = 0; r < RW; ++r) uu[r] = ldg4(p.U + (size_t)(wave + 4 * r) * ld + cc);   // rows < 16 <= Ip
-  asm volatile("" ::: "memory");   // keep those loads ahead of the M loads (in-order vmcnt)
-  // M rows k0 .. k0 + 31, columns col .. col + 3 (clamped when out of range; the
-  // products are then multiplied by P = 0, or the columns are never stored)
-  float4 m[32];
-  {
-    const float* src = p.M + (size_t)min(k0, ld - 32) * ldm + cc;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) m[j] = ldg4(src + (size_t)j * ldm);
-  }
-  wait_vmcnt<32>();   // P, flag, residuals and U are in; the 32 M rows stay in flight
-  __builtin_amdgcn_sched_barrier(0);   // nothing that reads them is scheduled above the wait
-  if (done) return;
-  if (iter > 0) {   // stop test (source/admm.py:59-65), uniform over the problem's units
-    double t = rv;
-    t += __shfl_xor(t, 4); t += __shfl_xor(t, 8); t += __shfl_xor(t, 16);   // lanes k = 0..3: sum k
-    const double t0 = __shfl(t, 0), t1 = __shfl(t, 1), t2 = __shfl(t, 2), t3 = __shfl(t, 3);
-    if (t0 / t1 < (double)eps && t2 / t3 < (double)eps) {
-      if (u.first && tid == 0) p.flags[0] = 1;   // sticky "break"
-      return;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < PJ; ++j) {
-    const int i = pi0 + 2 * j;
-    if (i < PS) Pt[pk][i] = (i < I && kb + pk < ld) ? pv[j] : 0.f;
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the transpose is written
-  raw_barrier();                        // (no vmcnt wait: the M rows stay in flight)
-  // acc[i] = {columns (x, y), (z, w)} of row i; packed FMAs (v_pk_fma_f32), k ascending
-  f2 acc[NR][2];
-#pragma unroll
-  for (int i = 0; i < NR; ++i) acc[i][0] = acc[i][1] = f2{0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const float* pt = &Pt[32 * wave + j][0];
-    float ps[PS];
-#pragma unroll
-    for (int q = 0; q < PS / 4; ++q) {
-      const float4 p4 = *reinterpret_cast<const float4*>(pt + 4 * q);
-      ps[4 * q] = p4.x; ps[4 * q + 1] = p4.y; ps[4 * q + 2] = p4.z; ps[4 * q + 3] = p4.w;
-    }
-    const f2 mxy = {m[j].x, m[j].y}, mzw = {m[j].z, m[j].w};
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const f2 pp = {ps[i], ps[i]};
-      acc[i][0] = __builtin_elementwise_fma(mxy, pp, acc[i][0]);
-      acc[i][1] = __builtin_elementwise_fma(mzw, pp, acc[i][1]);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NR; ++i)
-    *reinterpret_cast<float4*>(&red[wave][i][4 * lane]) = make_float4(acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y);
-  __syncthreads();
-  if (u.first) {   // this iteration's quantizer-search accumulators start at zero
-                   // (behind the barrier: no wait on the M rows behind these stores;
-                   // global-typed: a flat store may alias LDS and would pin the Pt reads)
-    typedef __attribute__((address_space(1))) unsigned long long gu64;
-    gu64* sse = (gu64*)(p.mv.sse + (size_t)slot * ncand);
-    gu64* h1 = (gu64*)(p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1));
-    gu64* h2 = (gu64*)(p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1));
-    for (int c = tid; c < ncand; c += 256) sse[c] = 0ull;
-    for (int c = tid; c < kHistRep * (ncand + 1); c += 256) { h1[c] = 0ull; h2[c] = 0ull; }
-    if (tid == 0) {
-      *(__attribute__((address_space(1))) double*)(p.mv.s2 + slot) = 0.0;
-      *(__attribute__((address_space(1))) unsigned*)(p.mv.ticket + slot) = 0u;
-    }
-  }
-  // wave w now owns rows w, w + 4, ...: block sum in wave order
-  float4 v[RW];
-#pragma unroll
-  for (int r = 0; r < RW; ++r) {
-    const int i = min(wave + 4 * r, NR - 1);   // rows >= NR: never stored
-    float4 a = *reinterpret_cast<const float4*>(&red[0][i][4 * lane]);
-#pragma unroll
-    for (int w = 1; w < 4; ++w) {
-      const float4 b = *reinterpret_cast<const float4*>(&red[w][i][4 * lane]);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-    v[r] = a;
-  }
-  if (u.nkg > 1) {
-    // The partial slab is handed over write-through (16-B sc1 buffer stores, drained
-    // before the counter add) and read back by the last block with sc1 buffer loads only,
-    // so no agent-scope acquire (an L1 invalidate, ~1.7 us on the last block's path) is
-    // needed (cdna_hip_programming.md Guideline 16, sc1 consumer).
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t prs =
-        __builtin_amdgcn_make_buffer_rsrc(p.Part, 0, (int)((size_t)u.nkg * NR * ld * sizeof(float)), 0x00020000);
-    if (cok) {
-#pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        if (wave + 4 * r >= NR) continue;
-        const int off = (int)((((size_t)u.kg * NR + wave + 4 * r) * ld + col) * sizeof(float));
-        const u32x4 w = {__float_as_uint(v[r].x), __float_as_uint(v[r].y), __float_as_uint(v[r].z),
-                         __float_as_uint(v[r].w)};
-        __builtin_amdgcn_raw_buffer_store_b128(w, prs, off, 0, 16);   // aux 16: sc1 (write-through)
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // this thread's partial stores are complete
-    __syncthreads();                 // ... and every thread's
-    if (tid == 0) {
-      unsigned* cnt = p.tcnt + u.cb;
-      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old + 1 == (unsigned)u.nkg;
-      if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // only keeps the sc1 loads below the ticket
-    // sum the nkg partials in kg order, 8 reduction blocks' loads in flight at a time
-#pragma unroll
-    for (int r = 0; r < RW; ++r) v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g0 = 0; g0 < u.nkg; g0 += 8) {
-      float4 t[8][RW];
-#pragma unroll
-      for (int gg = 0; gg < 8; ++gg) {
-        const int g = min(g0 + gg, u.nkg - 1);
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          const int off = (int)((((size_t)g * NR + min(wave + 4 * r, NR - 1)) * ld + cc) * sizeof(float));
-          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 16);   // sc1
-          t[gg][r] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
-        }
-      }
-#pragma unroll
-      for (int gg = 0; gg < 8; ++gg) {
-        const bool ok = g0 + gg < u.nkg;   // select, not a branch: the loads stay batched
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          v[r].x += ok ? t[gg][r].x : 0.f; v[r].y += ok ? t[gg][r].y : 0.f;
-          v[r].z += ok ? t[gg][r].z : 0.f; v[r].w += ok ? t[gg][r].w : 0.f;
-        }
-      }
-    }
-  }
-  // epilogue: HT, X = HT - U for the rows < I; stats of the valid region
-  unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
-  {
-    typedef __attribute__((address_space(1))) f32x4 gst4;
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int row = wave + 4 * r;
-      const float hs[4] = {v[r].x, v[r].y, v[r].z, v[r].w}, us[4] = {uu[r].x, uu[r].y, uu[r].z, uu[r].w};
-      f32x4 x4, h4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float xv = hs[c] - us[c];
-        x4[c] = xv; h4[c] = hs[c];
-        if (row < I && col + c < p.R) {
-          amax = max(amax, __float_as_uint(xv) & 0x7FFFFFFFu);
-          const unsigned e = enc_ord(xv);
-          mn = min(mn, e);
-          mxo = max(mxo, e);
-        }
-      }
-      if (cok && row < I) {
-        const size_t off = (size_t)row * ld + col;
-        *(gst4*)(p.HT + off) = h4;
-        if (p.X_dbg) *(gst4*)(p.X + off) = x4;
-      }
-    }
-  }
-  amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
-  if (lane == 0) {
-    unsigned* st = p.mv.stat + 4 * slot;
-    atomicMax(&st[0], amax);
-    atomicMin(&st[1], mn);
-    atomicMax(&st[2], mxo);
-  }
-}
-
 void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hipStream_t s) {
   if (nprob > 0 && maxrows > 0) hipLaunchKernelGGL(k_split_rows, dim3(maxrows, nprob), dim3(256), 0, s, d, which);
 }
@@ -892,19 +669,5 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
 #undef ADMMQ_GEMM
 }
 
-void launch_gemm_thin(const ProbDesc* d, const ThinUnit* units, int nunits, int nr, int slot, int iter, float eps,
-                      int ncand, hipStream_t s) {
-  if (nunits <= 0) return;
-  // nr: the largest thin factor height of the batch (exact: 9 for 3x3 kernels)
-#define ADMMQ_THIN(N) \
-  case N: hipLaunchKernelGGL(k_gemm_thin<N>, dim3(nunits), dim3(256), 0, s, d, units, slot, iter, eps, ncand); break
-  switch (nr) {
-    ADMMQ_THIN(1); ADMMQ_THIN(2); ADMMQ_THIN(3); ADMMQ_THIN(4); ADMMQ_THIN(5); ADMMQ_THIN(6); ADMMQ_THIN(7);
-    ADMMQ_THIN(8); ADMMQ_THIN(9); ADMMQ_THIN(10); ADMMQ_THIN(11); ADMMQ_THIN(12); ADMMQ_THIN(13); ADMMQ_THIN(14);
-    ADMMQ_THIN(15);
-    default: hipLaunchKernelGGL(k_gemm_thin<16>, dim3(nunits), dim3(256), 0, s, d, units, slot, iter, eps, ncand); break;
-  }
-#undef ADMMQ_THIN
-}
 
 }  // namespace admmq

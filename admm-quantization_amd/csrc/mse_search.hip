@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "quant_device.h"
+#include "search_device.h"
 
 namespace admmq {
 
@@ -89,38 +90,6 @@ int copy_sel_stats(unsigned long long* host, int reset) {
   return 3;
 }
 
-// Closed form of level_threshold(s, k) (s > 0 normal, k >= 1): rint(fl(a/s)) >= k
-// <=> fl(a/s) >= H with H = k - 1/2 (k even: rint(H) = k) or H = next float above
-// k - 1/2 (k odd: the tie rounds down). fl(a/s) >= H <=> a/s >= m, the midpoint of
-// H and the float below it, where a/s == m rounds to H iff H's last mantissa bit is
-// 0 (round half to even). s * m is exact in fp64 (24 + 25 significant bits), so the
-// threshold is the smallest float >= s m, one float higher on a tie that rounds
-// down. Checked against level_threshold by admmq_debug_check_thresholds.
-__device__ __forceinline__ float level_threshold_fast(float s, int k) {
-  float H = (float)k - 0.5f;
-  if (k & 1) H = __uint_as_float(__float_as_uint(H) + 1u);
-  const float Hm = __uint_as_float(__float_as_uint(H) - 1u);
-  const double m = 0.5 * ((double)H + (double)Hm);
-  const double prod = (double)s * m;
-  float a = (float)prod;                                   // round to nearest
-  if ((double)a < prod) a = __uint_as_float(__float_as_uint(a) + 1u);
-  else if ((double)a > prod) {                             // nearest went up: is the float below still >= prod?
-    const float b = __uint_as_float(__float_as_uint(a) - 1u);
-    if ((double)b >= prod) a = b;
-  }
-  if ((double)a == prod && (__float_as_uint(H) & 1u)) a = __uint_as_float(__float_as_uint(a) + 1u);
-  return a;
-}
-
-// Threshold table of one job into LDS: thr[(k-1) n + c] = smallest a with
-// |q_c(a)| >= k, for k = 1..qmax (increasing in c and in k).
-__device__ __forceinline__ void fill_thresholds(float* thr, float mx, int n, int qmax, int nt) {
-  const float den = (float)(2 * qmax - 1);
-  for (int e = threadIdx.x; e < qmax * n; e += nt) {
-    const int k = 1 + e / n, c = e - (k - 1) * n;
-    thr[e] = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
-  }
-}
 
 // Diagnostics: level_threshold_fast == level_threshold over random (s, k).
 __global__ void k_check_thresholds(unsigned seed, int nsamp, unsigned* mismatches) {
@@ -182,13 +151,7 @@ int check_thresholds(unsigned seed, int nsamp) {
   return ok ? (int)h : -1;
 }
 
-__device__ __forceinline__ int hist_fixed_exp(float mx, long long nelem, int qmax) {
-  int emx;
-  (void)__builtin_frexpf(mx, &emx);
-  const long long nterm = nelem * qmax;
-  const int clt = 64 - __builtin_clzll((unsigned long long)(nterm > 1 ? nterm - 1 : 1));
-  return 61 - emx - clt;
-}
+
 
 // Candidate selection for one job from the summed stage-1 histograms H1/H2 (LDS,
 // n+1 bins) and S2, by one wave. Lane l owns candidates [l P, l P + P), P = ceil(n/64);
@@ -196,25 +159,6 @@ __device__ __forceinline__ int hist_fixed_exp(float mx, long long nelem, int qma
 // block, walked downwards). A(c) = S2 - 2 s T1 + s^2 T2 with E(c) its rigorous error
 // bound (oracle/stage1_model.py); pass 1 finds min(A + E), pass 2 writes
 // S = {c : A - E <= min(A + E)} in ascending order (prefix count over lanes).
-struct SelCtx {
-  double S2, fixu, u, Kterm, Nterm, tiny;
-  float mx, denf;
-  int n;
-  __device__ void bounds(int c, unsigned long long T1i, unsigned long long T2i, double& lo, double& hi) const {
-    const double s = (double)((2.0f * cand_t(mx, c, n)) / denf);
-    const double T1 = (double)T1i * fixu;
-    const double T2 = (double)T2i;
-    const double A = S2 - 2.0 * s * T1 + s * s * T2;
-    const double mag = S2 + 2.0 * s * T1 + s * s * T2;
-    const double slack = 1e-10 * mag;
-    const double sh = fmax(A, 0.0) + slack;
-    const double B1 = 2.0 * u * (1.0 + u) * (s * sqrt(T2 * sh) + sh) + 2.0 * u * u * (1.0 + u) * (1.0 + u) * (s * s * T2 + sh);
-    const double E = B1 + 3.0000002 * u * (sh + B1) + Kterm + 2.0 * s * Nterm * fixu + slack + tiny;
-    lo = A - E;
-    hi = A + E;
-  }
-};
-
 __device__ void select_wave(const MseView& v, int* sel, int* lsel, const unsigned long long* H1,
                             const unsigned long long* H2, double S2, float mx, int n, int qmax) {
   const int lane = threadIdx.x & 63;
@@ -368,52 +312,7 @@ __global__ __launch_bounds__(1024, 8) void k_mse_hist(const ProbDesc* __restrict
   for (int j = 0; j < 4 * NV; ++j) {
     const float4 q4 = x4v[j >> 2];
     const float x = (j & 3) == 0 ? q4.x : ((j & 3) == 1 ? q4.y : ((j & 3) == 2 ? q4.z : q4.w));
-    s2 += (double)x * (double)x;
-    const float a = __builtin_fabsf(x);
-    const int cap = (x > 0.f) ? QMAX - 1 : QMAX;
-    int k0 = 0, kfull = 0;
-#pragma unroll
-    for (int k = 1; k <= QMAX; ++k) {
-      k0 += (k <= cap && a >= tlo0[k - 1]) ? 1 : 0;
-      kfull += (k <= cap && a >= thin[k - 1]) ? 1 : 0;
-    }
-    if (x == 0.f) k0 = 0;
-    const unsigned long long af = to_fixed(a, K1);
-    full1 += af * (unsigned long long)kfull;
-    full2 += (unsigned)(kfull * kfull);              // sum_{k<=kfull} (2k-1)
-    // levels kfull < k <= k0 have a breakpoint b in [1, n-1]: a linear estimate (off by at
-    // most one) checked against its two neighbouring thresholds; exact -> add now (inactive
-    // lanes add 0 to their private dummy bin, no branch); off -> the rare exact search below
-    unsigned slow = 0u;
-#pragma unroll
-    for (int k = 1; k <= QMAX; ++k) {
-      const bool act = (k > kfull && k <= k0);
-      const float tau = a * ((float)(2 * QMAX - 1) / (float)(2 * k - 1));   // estimate only
-      const float ce = (tau - S0) * inv_step;
-      int b = (ce >= (float)(n - 1)) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
-      b = max(min(b, n - 1), 1);
-      const float* tk = thr + (k - 1) * n;
-      const bool exact = (a >= tk[b - 1]) && (a < tk[b]);
-      const bool add = act && exact;
-      slow |= (act && !exact) ? (1u << k) : 0u;
-      const int bin = add ? b : dummy;
-      atomicAdd(&h1[bin], add ? af : 0ull);
-      atomicAdd(&h2[bin], add ? (unsigned)(2 * k - 1) : 0u);
-    }
-    if (slow) {   // rare: exact breakpoint by binary search (largest b with thr[k][b-1] <= a)
-#pragma unroll 1
-      for (int k = 1; k <= QMAX; ++k) {
-        if (!((slow >> k) & 1u)) continue;
-        const float* tk = thr + (k - 1) * n;
-        int lo = 1, hi = n - 1;   // a >= tk[0] and a < tk[n-1]: answer in [1, n-1]
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (a >= tk[mid - 1]) lo = mid; else hi = mid - 1;
-        }
-        atomicAdd(&h1[lo], af);
-        atomicAdd(&h2[lo], (unsigned)(2 * k - 1));
-      }
-    }
+    hist_insert_elem<QMAX>(x, thr, n, S0, inv_step, K1, dummy, tlo0, thin, h1, h2, s2, full1, full2);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1020,10 +919,31 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   if (mse_degenerate(mx)) {     // the projection emits NaN for degenerate mx (no search)
     if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
     if constexpr (FIN) {
-      load_hf();
       const ProbDesc& p = d[ck.job];
-      admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qparams_mse(bits, __builtin_nanf("")),
-                                              slot, iter, blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+      const int nu = max(ck.reps, 1);
+      for (int r = 0; r < nu; ++r) {   // every unit of the block (several: re-read its elements)
+        const long long ub = (long long)ck.start + (long long)r * ck.step;
+        const long long ue = nu > 1 ? min(ub + ck.step, total) : total;
+        if (nu > 1) {
+#pragma unroll
+          for (int hh = 0; hh < 2 * NV; ++hh) {
+            const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
+            const long long ec = e < ue ? e : 0;
+            x4[hh] = gld4(ck.X + ec);
+            u4[hh] = gld4(ck.U + ec);
+          }
+        }
+#pragma unroll
+        for (int hh = 0; hh < 2 * NV; ++hh) {
+          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
+          const long long ec = e < ue ? e : 0;
+          h4[hh] = gld4(ck.H + ec);
+          f4[hh] = gld4(ck.F + ec);
+        }
+        if (r > 0) __syncthreads();
+        admm_finalize_block<kH3Threads, 2 * NV>(p, ub, ue, x4, u4, h4, f4, qparams_mse(bits, __builtin_nanf("")), slot,
+                                                iter, blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+      }
     }
     return;
   }
@@ -1043,9 +963,10 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
   const int dummy = M + 1 + (threadIdx.x & 63);
   double s2 = 0.0;
-  // without the fused finalize a block may take several consecutive units of its job
-  // (ck.reps, `step` elements each): one table setup and one flush for all of them
-  const int reps = FIN ? 1 : max(ck.reps, 1);
+  // a block may take several consecutive units of its job (ck.reps, `step` elements each):
+  // one table setup and one flush for all of them (FIN: only when the launch has more
+  // units than resident blocks; the finalize then re-reads each unit's elements)
+  const int reps = max(ck.reps, 1);
   for (int r = 0; r < reps; ++r) {
     const long long ub = (long long)ck.start + (long long)r * ck.step;   // unit r (r > 0: reps > 1 only)
     const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
@@ -1163,7 +1084,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   }
   if constexpr (FIN) {
     const ProbDesc& p = d[ck.job];
-    load_hf();
+    if (reps == 1) load_hf();   // (several units: re-read per unit below)
     if (!last) {   // wait for the job's selection (bounded)
       if (threadIdx.x == 0) {
         unsigned polls = 0;
@@ -1199,9 +1120,28 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     }
     __syncthreads();   // the search tables' LDS is reused as rmax
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) g_hist_trace[blockIdx.x][5] = ADMMQ_NOW();
-    admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
-                                            blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem),
-                                            ADMMQ_TRACE && blockIdx.x < kHistTraceMax ? g_fin_trace[blockIdx.x] : nullptr);
+    if (reps == 1) {
+      admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
+                                              blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem),
+                                              ADMMQ_TRACE && blockIdx.x < kHistTraceMax ? g_fin_trace[blockIdx.x] : nullptr);
+    } else {
+      for (int r = 0; r < reps; ++r) {   // each unit's H_T, U, H, F again (L2-resident), then its finalize step
+        const long long ub = (long long)ck.start + (long long)r * ck.step;
+        const long long ue = min(ub + ck.step, total);
+#pragma unroll
+        for (int hh = 0; hh < 2 * NV; ++hh) {
+          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
+          const long long ec = e < ue ? e : 0;
+          x4[hh] = gld4(ck.X + ec);
+          u4[hh] = gld4(ck.U + ec);
+          h4[hh] = gld4(ck.H + ec);
+          f4[hh] = gld4(ck.F + ec);
+        }
+        __syncthreads();   // rmax / the reduction scratch of the previous unit are free again
+        admm_finalize_block<kH3Threads, 2 * NV>(p, ub, ue, x4, u4, h4, f4, qp, slot, iter, blockIdx.x & (kResRep - 1),
+                                                reinterpret_cast<unsigned*>(smem), nullptr);
+      }
+    }
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
       // columns 4, 5: {wait for the selection done, finalize done} (the search ended at 3 / 4)
       const unsigned long long tw = g_hist_trace[blockIdx.x][5];

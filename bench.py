@@ -135,7 +135,7 @@ def reduce_over_ranks(elapsed, factor_iters, world, device):
 
 PEAK_F16_MFMA = 16 * PEAK_F32  # TFLOP/s dense f16 MFMA (MI355X_MICROARCH.md: 1/16 rate ratio, ~2.5 PF)
 PEAK_HBM = 8.0                 # TB/s HBM3E spec
-THIN_ROWS = 16                 # kThinRows: factors with I <= 16 take k_gemm_thin / k_mse_small_admm
+THIN_ROWS = 16                 # kThinRows: factors with I <= 16 take k_thin_solve / k_mse_small_admm or k_thin_loop
 SPLIT_PRODUCTS = 3             # split-fp16 solve: Ph Mh + Ph Ml + Pl Mh per solve flop
 
 # Launch classes of admmq_profile_end (include/admmq.h ADMMQ_PROF_*) and, per element of
@@ -149,10 +149,15 @@ SPLIT_PRODUCTS = 3             # split-fp16 solve: Ph Mh + Ph Ml + Pl Mh per sol
 #                     per element; reported beside the byte roofline as `valu_equiv`)
 #   small             search + finalize of the I <= 16 factors in one block: 8 I R + 28 I R B
 #   finalize          read H_T, H, U, F, write H, U, next P: 28 I R B
-PROF_CLASSES = ["gemm", "gemm_thin", "search", "small", "finalize", "prepare"]
-KERNEL_NAMES = {"gemm": "k_gemm (solve, split-f16 MFMA)", "gemm_thin": "k_gemm_thin (solve, I<=16, VALU)",
+#   thin_loop         every iteration of an all-thin call in one launch (k_thin_loop):
+#                     (max_iter - 1) x 2 I R^2 solve flops; compulsory HBM bytes once per
+#                     call: M, F, H, U, P in, H, U out: 4 (R^2 + 6 I R) B
+PROF_CLASSES = ["gemm", "gemm_thin", "search", "small", "finalize", "prepare", "thin_loop"]
+PER_ITER_CLASSES = PROF_CLASSES[:5]
+KERNEL_NAMES = {"gemm": "k_gemm (solve, split-f16 MFMA)", "gemm_thin": "k_thin_solve (solve, I<=16, VALU)",
                 "search": "k_mse_hist3 (two-stage MSE search)", "small": "k_mse_small_admm (I<=16 search+finalize)",
-                "finalize": "k_finalize_admm (projection + dual update)", "prepare": "prepare (rho, SPD inverse, planes)"}
+                "finalize": "k_finalize_admm (projection + dual update)", "prepare": "prepare (rho, SPD inverse, planes)",
+                "thin_loop": "k_thin_loop (persistent: every iteration of the I<=16 factors, VALU solve)"}
 
 
 def mode_problems(work):
@@ -162,12 +167,18 @@ def mode_problems(work):
     return [[(s.shape[m], R) for (s, _, R, _) in work if m < len(s.shape)] for m in range(nm)]
 
 
-def class_work(work, num_attempts=200, split=True, fused=False):
+def class_work(work, num_attempts=200, split=True, fused=False, max_iter_admm=1000):
     """Per launch class: (flops, bytes, valu_equiv_flops) of ONE launch, averaged over the
     modes whose calls issue it. The HIP-event sampling times one iteration in N of every
     mode call, so each issuing mode weighs equally in the measured average duration."""
     out = {}
-    for cls in PROF_CLASSES[:5]:
+    loop = [[(i, r) for (i, r) in probs] for probs in mode_problems(work) if all(i <= THIN_ROWS for (i, _) in probs)]
+    if loop:
+        n = len(loop)
+        out["thin_loop"] = (sum((max_iter_admm - 1) * 2.0 * i * r * r for p in loop for (i, r) in p) / n,
+                            sum(4.0 * (r * r + 6 * i * r) for p in loop for (i, r) in p) / n,
+                            sum((max_iter_admm - 1) * 8.0 * num_attempts * i * r for p in loop for (i, r) in p) / n)
+    for cls in PER_ITER_CLASSES:
         per_mode = []
         for probs in mode_problems(work):
             big = [(i, r) for (i, r) in probs if i > THIN_ROWS]
@@ -468,18 +479,22 @@ def main():
             avg_us = {c: 1e3 * ms[i] / cnt[i] for i, c in enumerate(PROF_CLASSES) if cnt[i]}
             traffic = load_traffic(a.model, split)
             fused = "search" in avg_us and "finalize" not in avg_us   # the big jobs' finalize ran in the search launch
-            cw = class_work(work, split=split, fused=fused)
+            cw = class_work(work, split=split, fused=fused, max_iter_admm=a.max_iter_admm)
             rf = {c: kernel_roofline(c, cw[c], avg_us[c], cnt[i], split, traffic)
-                  for i, c in enumerate(PROF_CLASSES[:5]) if c in cw and c in avg_us}
+                  for i, c in enumerate(PROF_CLASSES) if c in cw and c in avg_us}
             if fused and "search" in rf:
                 rf["search"]["kernel"] = "k_mse_hist3 (two-stage MSE search + fused finalize)"
             # per step: each class launches once per inner iteration of every mode that issues it
-            n_issuing = {c: sum(1 for probs in mode_problems(work)
+            # (all-thin calls run as one k_thin_loop launch instead: per call, every call timed)
+            per_iter_modes = [p for p in mode_problems(work) if not (cnt[PROF_CLASSES.index("thin_loop")] and
+                                                                     all(i <= THIN_ROWS for (i, _) in p))]
+            n_issuing = {c: sum(1 for probs in per_iter_modes
                                 if any((i <= THIN_ROWS) == (c in ("gemm_thin", "small")) for (i, _) in probs))
-                         for c in PROF_CLASSES[:5]}
-            per_step = {c: avg_us[c] * 1e-3 * n_issuing[c] * (a.max_iter_admm - 1) for c in rf}
-            if "prepare" in avg_us:
-                per_step["prepare"] = avg_us["prepare"] * 1e-3 * cnt[PROF_CLASSES.index("prepare")] / a.steps
+                         for c in PER_ITER_CLASSES}
+            per_step = {c: avg_us[c] * 1e-3 * n_issuing[c] * (a.max_iter_admm - 1) for c in rf if c in n_issuing}
+            for c in ("prepare", "thin_loop"):
+                if c in avg_us:
+                    per_step[c] = avg_us[c] * 1e-3 * cnt[PROF_CLASSES.index(c)] / a.steps
             dom = max(rf, key=lambda c: per_step[c])
             out["roofline"] = rf[dom]
             out["roofline_kernels"] = rf

@@ -167,7 +167,9 @@ int32_t admmq_get_solve_mode(void);
  * (k_mse_hist3 / k_mse_hist / the exhaustive sweep), ADMMQ_PROF_SMALL k_mse_small_admm
  * (search + projection + dual update of the I <= 16 factors in one block each),
  * ADMMQ_PROF_FINALIZE k_finalize_admm (projection + dual update), ADMMQ_PROF_PREPARE the
- * whole prepare phase (rho, SPD inverse, operand planes). Only ADMM iterations it with
+ * whole prepare phase (rho, SPD inverse, operand planes), ADMMQ_PROF_THIN_LOOP k_thin_loop
+ * (every iteration of a call whose factors all have I <= 16, one persistent launch, always
+ * timed). Only ADMM iterations it with
  * it % sample_every == 0 are timed (each event pair adds an inter-kernel gap, so the
  * bench samples instead of timing every launch). end() synchronises on the last event
  * and fills ADMMQ_PROF_CLASSES summed milliseconds and launch counts. */
@@ -177,6 +179,7 @@ int32_t admmq_get_solve_mode(void);
 #define ADMMQ_PROF_SMALL 3
 #define ADMMQ_PROF_FINALIZE 4
 #define ADMMQ_PROF_PREPARE 5
+#define ADMMQ_PROF_THIN_LOOP 6
 #define ADMMQ_PROF_CLASSES 8
 int32_t admmq_profile_begin(int32_t max_launches, int32_t sample_every);
 int32_t admmq_profile_end(double* ms_per_class, int64_t* launches_per_class);

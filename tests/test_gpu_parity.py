@@ -208,11 +208,13 @@ def test_reference_fixture_short_horizon(torch_dev):
     assert _rel(H.cpu().numpy(), z["w2_it3_H"]) < 1e-4
 
 
-@pytest.mark.parametrize("I,R", [(1, 40), (3, 300), (5, 129), (9, 700), (12, 257), (16, 1100), (17, 200)])
+@pytest.mark.parametrize("I,R", [(1, 40), (3, 300), (5, 129), (9, 700), (12, 257), (16, 1100), (9, 1500), (16, 2400),
+                                 (17, 200)])
 def test_thin_factor_solve(torch_dev, I, R):
-    """Factors with I <= 16 rows take the VALU split-K solve (k_gemm_thin, exact row
-    count, 128-row reduction blocks summed by the last block to arrive); I = 17 takes
-    the 32-row MFMA tiles. One step vs the oracle, batched with a tall factor."""
+    """Factors with I <= 16 rows take the VALU solve of thin_loop.hip (k_thin_solve: 32
+    columns per workgroup, M in registers, the canonical class-chain order; ld > 1152 in
+    several reduction chunks); I = 17 takes the 32-row MFMA tiles. One step vs the
+    oracle, batched with a tall factor (so the per-iteration path runs)."""
     torch, dev = torch_dev
     from admmq import admm_iteration_batched
     rng = np.random.default_rng(I * 1000 + R)
@@ -417,6 +419,71 @@ def test_fused_finalize_equals_separate(torch_dev, eps):
         assert np.array_equal(ia, ib)
         for (ha, ua), (hb, ub) in zip(a, b):
             assert _bits_equal(ha, hb) and _bits_equal(ua, ub)
+    # the fused finalize with several units per block (a launch with more units than
+    # resident blocks, e.g. C4): forced here by a small resident-block budget
+    for cap in (60, 25):
+        with _lib.fin_capacity(cap):
+            c, ic = run(True)
+        assert (ic[:, 3] == 0).all() and np.array_equal(ia, ic)
+        for (ha, ua), (hc, uc) in zip(a, c):
+            assert _bits_equal(ha, hc) and _bits_equal(ua, uc)
+
+
+@pytest.mark.parametrize("eps,bits,na", [(0.0, 4, 200), (1e-3, 4, 200), (0.0, 2, 64), (0.0, 3, 256), (0.0, 5, 100)])
+def test_thin_loop_equals_per_iteration(torch_dev, eps, bits, na):
+    """A call whose factors are all thin (mode 2 of the 3x3 convs, I = 9) runs every
+    iteration in one persistent launch (k_thin_loop: M in registers, team barriers). It
+    gives the bits of the per-iteration launches (k_thin_solve + k_mse_small_admm): H, U
+    and the iteration counts (eps = 1e-3 exercises the team's stop test), with no internal
+    fault; 2..5 bits and 64..256 candidates."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    probs_np = [_layer_problem(l, 2) for l in ("layer1.0.conv1", "layer2.1.conv1", "layer3.1.conv2", "layer4.1.conv2",
+                                               "layer4.0.conv1")]
+
+    def run(loop):
+        ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+              for H, F, G in probs_np]
+        with _lib.thin_loop(loop):
+            Hs, info = admm_iteration_batched(ps, 12, eps, bits, MSE, num_attempts=na, return_info=True)
+        return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
+
+    a, ia = run(True)
+    b, ib = run(False)
+    assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
+    assert np.array_equal(ia, ib), (ia, ib)
+    for (ha, ua), (hb, ub) in zip(a, b):
+        assert _bits_equal(ha, hb) and _bits_equal(ua, ub)
+    if eps == 0.0:
+        assert (ia[:, 0] == 11).all()
+
+
+def test_thin_loop_one_step_vs_oracle(torch_dev):
+    """One step of the persistent loop against the oracle: H_T within 1e-5, the projection
+    and the dual update bit-exact given the kernel's own H_T (P2), for I = 1..16 thin
+    factors in one call (the 16-row instance of the loop)."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    rng = np.random.default_rng(77)
+    probs, ref, U0s = [], [], []
+    for (i, r) in [(9, 700), (16, 1100), (1, 40), (5, 129)]:
+        B = rng.standard_normal((r, 2 * r)).astype(np.float32) / np.float32(np.sqrt(2 * r))
+        G = (B @ B.T + 0.5 * np.eye(r)).astype(np.float32)
+        F = rng.standard_normal((i, r)).astype(np.float32)
+        H0 = (rng.standard_normal((i, r)) * 0.1).astype(np.float32)
+        U0 = (rng.standard_normal((i, r)) * 0.01).astype(np.float32)
+        U0s.append(U0)
+        probs.append((_t(torch, dev, H0), _t(torch, dev, U0), _t(torch, dev, F), _t(torch, dev, G)))
+        ref.append(ao.admm_iteration(H0, U0, F, G, 2, 1e-8, 4, MSE, return_info=True)[2])
+    Hs, dbg, info = admm_iteration_batched(probs, 2, 1e-8, 4, MSE, debug_outputs=True, return_info=True)
+    assert int(info[:, 3].max()) == 0
+    for H, (HT, X), p, U0, inf in zip(Hs, dbg, probs, U0s, ref):
+        HT, X = HT.cpu().numpy(), X.cpu().numpy()
+        assert _rel(HT, inf["HT"]) < 1e-5
+        assert _bits_equal(X, (HT - U0).astype(np.float32))
+        Hq = qo.quantize_tensor(X, 4, MSE)
+        assert _bits_equal(H.cpu().numpy(), Hq)
+        assert _bits_equal(p[1].cpu().numpy(), (U0 + (Hq - HT).astype(np.float32)).astype(np.float32))
 
 
 def test_fused_finalize_timeout_reported_and_repaired(torch_dev):
@@ -479,6 +546,43 @@ def test_fused_finalize_timeout_reported_and_repaired(torch_dev):
         assert int(inf[:, 3].max()) == 0
         for (hr, ur), h, p in zip(ref, Hs, ps):
             assert _bits_equal(hr, h.cpu().numpy()) and _bits_equal(ur, p[1].cpu().numpy())
+
+    # the persistent thin-factor loop's bounded team barriers: one poll times out, the call
+    # reports it, and the op re-runs it with the per-iteration launches
+    thin_np = [_layer_problem(l, 2) for l in ("layer4.1.conv2", "layer1.0.conv1")]
+
+    def mk_thin():
+        return [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+                for H, F, G in thin_np]
+
+    ref_ps = mk_thin()
+    with _lib.thin_loop(False):
+        ref_H = admm_iteration_batched(ref_ps, 8, 0.0, 4, MSE)
+    ps = mk_thin()
+    items = [_problem(H, U, F, G) for H, U, F, G in ps]
+    for it, p in zip(items, ps):
+        it.H_out = torch.empty_like(p[0]).data_ptr()
+    arr = _lib.problems_array(items)
+    nb = lib.admmq_admm_workspace_size_ex(arr, len(items), 200, po)
+    ws = _lib.workspace(nb, dev)
+    info = torch.zeros(len(items) * 4, dtype=torch.int32, device=dev)
+    _lib.check(lib.admmq_admm_prepare_ex(arr, len(items), 200, po, _lib.ptr(ws), nb, st), "prepare")
+    with _lib.fin_wait_polls(1):
+        _lib.check(lib.admmq_admm_run_ex(arr, len(items), 8, 0.0, 4, 0, 200, po, _lib.ptr(ws), nb, _lib.ptr(info), st),
+                   "run")
+    torch.cuda.synchronize()
+    assert int(info.view(-1, 4)[:, 3].max()) != 0, "a one-poll team barrier should have timed out"
+    for route in ("ops", "cabi"):
+        ps = mk_thin()
+        with _lib.fin_wait_polls(1):
+            if route == "ops":
+                Hs, inf = admm_iteration_batched(ps, 8, 0.0, 4, MSE, return_info=True)
+            else:
+                Hs, inf = _admm_iteration_batched_cabi(ps, 8, 0.0, 4, 0, 200, False, False, True)
+        assert int(inf[:, 3].max()) == 0
+        for hr, pr, h, p in zip(ref_H, ref_ps, Hs, ps):
+            assert _bits_equal(hr.cpu().numpy(), h.cpu().numpy())
+            assert _bits_equal(pr[1].cpu().numpy(), p[1].cpu().numpy())
 
 
 @pytest.mark.parametrize("route", ["ops", "cabi"])

@@ -273,13 +273,16 @@ class fin_capacity:
 class thin_loop:
     """Context manager: the persistent loop of the thin factors (k_thin_loop: every
     iteration of a call whose factors all have I <= 16 in one launch; default on) or the
-    per-iteration launches. Restores the default on exit."""
+    per-iteration launches; ``"wide"``: on, with 64-column workgroups wherever allowed
+    (ld <= 512; normally only when 32-column teams would not fit on the CUs). Restores the
+    default on exit."""
 
-    def __init__(self, enable: bool):
+    def __init__(self, enable):
         self.enable = enable
 
     def __enter__(self):
-        check(load().admmq_debug_set_thin_loop(1 if self.enable else 0), "thin_loop")
+        code = 2 if self.enable == "wide" else (1 if self.enable else 0)
+        check(load().admmq_debug_set_thin_loop(code), "thin_loop")
         return self
 
     def __exit__(self, *exc):

@@ -222,6 +222,7 @@ int copy_gemm_trace(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
 int copy_fin_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);
+int copy_thin_loop_trace(unsigned long long* host, int n);
 int copy_sel_stats(unsigned long long* host, int reset);
 int check_thresholds(unsigned seed, int nsamp);
 int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out);

@@ -80,8 +80,9 @@ static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
 // to exercise its several-units-per-block form on small batches
 static std::atomic<int> g_fin_cap_override{0};
 // persistent loop of the thin factors (k_thin_loop) for calls whose problems are all
-// thin; off: the per-iteration launches (A/B and cross-check)
-static std::atomic<bool> g_thin_loop{true};
+// thin: 1 on, 0 off (the per-iteration launches: A/B and cross-check), 2 on with 64-column
+// workgroups wherever allowed (exercises that form on batches that fit without it)
+static std::atomic<int> g_thin_loop{1};
 
 // Tile rows of the persistent fp32 solve per problem (fixed by the problem's shape, never
 // by the batch, so every element's result is batch-independent): 0 = 64 x 64 tiles
@@ -301,8 +302,11 @@ struct AdmmPlan {
   bool rows_aligned = true;          // every big job's stage-1 units are whole rows (fused finalize possible)
   unsigned* d_ready = nullptr;       // [nprob][2] fused-finalize ready words (zeroed per run)
   int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
-  // persistent thin-factor loop (k_thin_loop, one team of `thin` workgroups per problem):
-  // possible when every problem is thin, ld <= 1152 and the workgroups fit the CUs
+  // persistent thin-factor loop (k_thin_loop, one team of workgroups per problem): possible
+  // when every problem is thin, ld <= 1152 and the workgroups fit the CUs (64-column
+  // workgroups for some ld <= 512 problems where 32-column ones would not)
+  std::vector<ThinLoopUnit> tl_units;
+  ThinLoopUnit* d_tl_units = nullptr;
   ThinSync* d_tl_sync = nullptr;
   bool tl_ok = false;
 };
@@ -368,6 +372,48 @@ static int fin_groups_for(const std::vector<ProbDesc>& desc, const std::vector<i
   int g = units4k >= kFinMinUnits ? 4 : 1;   // small problem sets keep their parallelism
   while (g < 8 && 1024 * g < maxld) g *= 2;
   return g;
+}
+
+// Teams of the persistent thin-factor loop: 32-column workgroups, and while they would
+// not all fit on the CUs at once, the shortest problems with ld <= 512 take 64-column ones
+// (two k classes per thread, the same chains and sums: thin_loop.hip), whose per-iteration
+// work (64 ld) stays below the largest team's (32 x 1152).
+static bool plan_thin_teams(AdmmPlan& pl, int ncu) {
+  pl.tl_units.clear();
+  const int nprob = (int)pl.desc.size();
+  if ((int)pl.small.size() != nprob || nprob == 0 || pl.thin_maxld > 1152) return false;
+  std::vector<int> cw(nprob, 32);
+  auto nwg = [&](int i) { const int ld = pl.desc[i].ld; return cw[i] == 64 ? ld / 64 + (ld % 64 ? 1 : 0) : ld / 32; };
+  long long total = 0;
+  for (int i = 0; i < nprob; ++i) total += nwg(i);
+  const bool wide_all = g_thin_loop.load() == 2;
+  while (total > ncu || wide_all) {
+    int best = -1;
+    for (int i = 0; i < nprob; ++i)
+      if (cw[i] == 32 && pl.desc[i].ld <= 512 && pl.desc[i].ld >= 64 && (best < 0 || pl.desc[i].ld < pl.desc[best].ld))
+        best = i;
+    if (best < 0) {
+      if (total > ncu) return false;
+      break;
+    }
+    total -= nwg(best);
+    cw[best] = 64;
+    total += nwg(best);
+  }
+  for (const ThinLoopUnit& u0 : pl.thin) {   // the problems in the planner's order
+    if (u0.col0 != 0) continue;
+    const int i = u0.job, ld = pl.desc[i].ld;
+    const int n = nwg(i);
+    for (int c = 0, r = 0; c < ld; ++r) {
+      const int w = std::min(cw[i], ld - c);
+      ThinLoopUnit u;
+      std::memset(&u, 0, sizeof(u));
+      u.job = i; u.col0 = c; u.cw = w; u.rank = r; u.nteam = n;
+      pl.tl_units.push_back(u);
+      c += w;
+    }
+  }
+  return true;
 }
 
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl, int solve_mode) {
@@ -648,7 +694,8 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_thin = cv.take<ThinLoopUnit>(pl.thin.size());
   if ((int)pl.small.size() == nprob) {   // sized by the problems alone (not by the device's CUs)
     pl.d_tl_sync = cv.take<ThinSync>(nprob);
-    pl.tl_ok = pl.thin_maxld <= 1152 && (int)pl.thin.size() <= device_cus();
+    pl.d_tl_units = cv.take<ThinLoopUnit>(pl.thin.size());   // >= the loop's workgroups
+    pl.tl_ok = plan_thin_teams(pl, device_cus());
   }
   pl.d_rank0 = cv.take<unsigned short>(kMaxMerged + kCells + 2);
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
@@ -846,9 +893,11 @@ int32_t admmq_debug_set_fin_capacity(int32_t blocks) {
   return ADMMQ_OK;
 }
 
-// diagnostics (not in include/admmq.h): the persistent thin-factor loop on / off
+// diagnostics (not in include/admmq.h): the persistent thin-factor loop on / off / on with
+// 64-column workgroups wherever allowed
 int32_t admmq_debug_set_thin_loop(int32_t on) {
-  g_thin_loop = on != 0;
+  if (on < 0 || on > 2) return fail(ADMMQ_ERR_ARG, "thin_loop: 0, 1 or 2");
+  g_thin_loop = on;
   return ADMMQ_OK;
 }
 
@@ -1060,13 +1109,14 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   // every problem thin: all iterations in one persistent launch (k_thin_loop) when the
   // fused paths are allowed (the op's fault retry turns them off) and it fits the device
   bool loop_done = false;
-  if (pl.tl_ok && g_thin_loop.load() && opt->fused_finalize && qscheme == kMse && !exhaustive && max_iter > 1 &&
+  if (pl.tl_ok && g_thin_loop.load() != 0 && opt->fused_finalize && qscheme == kMse && !exhaustive && max_iter > 1 &&
       num_attempts >= 2 && num_attempts <= kTLMaxCand && bits >= 2 && bits <= 5) {
+    if ((rc = h2d(pl.d_tl_units, pl.tl_units.data(), pl.tl_units.size() * sizeof(ThinLoopUnit), s))) return rc;
     if (hipMemsetAsync(pl.d_tl_sync, 0, (size_t)nprob * sizeof(ThinSync), s) != hipSuccess)
       return check_hip("thin loop reset");
     g_prof.sampled = true;
     prof_class(ADMMQ_PROF_THIN_LOOP); prof_mark(s);
-    loop_done = launch_thin_loop(pl.d_desc, pl.d_thin, (int)pl.thin.size(), pl.d_tl_sync, pl.thin_nr, pl.thin_maxld,
+    loop_done = launch_thin_loop(pl.d_desc, pl.d_tl_units, (int)pl.tl_units.size(), pl.d_tl_sync, pl.thin_nr, pl.thin_maxld,
                                  max_iter - 1, eps, num_attempts, bits, polls, device_cus(), s) == 0;
     prof_mark(s);
   }
@@ -1151,6 +1201,7 @@ int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return cop
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
 int32_t admmq_debug_fin_trace(unsigned long long* host, int32_t n) { return copy_fin_trace(host, n); }
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }
+int32_t admmq_debug_thin_loop_trace(unsigned long long* host, int32_t n) { return copy_thin_loop_trace(host, n); }
 int32_t admmq_debug_sel_stats(unsigned long long* host, int32_t reset) { return copy_sel_stats(host, reset); }
 int32_t admmq_debug_check_thresholds(uint32_t seed, int32_t nsamp) { return check_thresholds(seed, nsamp); }
 int32_t admmq_debug_check_cells(int32_t n, int32_t bits, uint32_t seed, int32_t nsamp, uint32_t* maxdev) {

@@ -620,15 +620,20 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
 #pragma unroll
   for (int j = 0; j < (kCellWords + 511) / 512; ++j)
     if (j < ncw) cv[j] = gld_u32(cw + min((int)threadIdx.x + j * nt, kCellWords - 1));
+  // the candidates' scales s_c = fl(2 t_c / den), one division each (not one per level and
+  // candidate), in LDS after the cell index (hist3_lds_bytes)
+  const float den = (float)(2 * QMAX - 1);
+  float* scand = reinterpret_cast<float*>(cell + kCells + 2);   // 4-B aligned: cell is, kCells + 2 is even
+  for (int c = threadIdx.x; c < n; c += nt) scand[c] = (2.0f * cand_t(mx, c, n)) / den;
+  __syncthreads();
   // thresholds, each also scattered to its host-order rank (kR0 * nt >= kMaxMerged >= M);
   // L = rank + 1 (tie groups below)
-  const float den = (float)(2 * QMAX - 1);
 #pragma unroll
   for (int j = 0; j < kR0; ++j) {
     const int e = threadIdx.x + j * nt;
     if (e < M) {
       const int k = 1 + e / n, c = e - (k - 1) * n;
-      const float v = level_threshold_fast((2.0f * cand_t(mx, c, n)) / den, k);
+      const float v = level_threshold_fast(scand[c], k);
       thr[e] = v;
       tsort[pre.r0v[j]] = v;
       rnk[e] = (unsigned short)(pre.r0v[j] + 1);
@@ -1297,7 +1302,7 @@ void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ng
 size_t hist3_lds_bytes(int ncand, int bits) {
   const size_t M = (size_t)ncand << (bits - 1);
   const size_t nb = M + 1 + 64;
-  const size_t bytes = nb * (8 + 8 + 4 + 4) + M * 8 + (((M + 1) & ~(size_t)1) + kCells + 2) * 2;
+  const size_t bytes = nb * (8 + 8 + 4 + 4) + M * 8 + (((M + 1) & ~(size_t)1) + kCells + 2) * 2 + (size_t)ncand * 4;
   return std::max((bytes + 15) & ~(size_t)15, (size_t)kSseQuads * 16);
 }
 

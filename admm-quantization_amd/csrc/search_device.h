@@ -54,7 +54,10 @@ struct SelCtx {
   float mx, denf;
   int n;
   __device__ void bounds(int c, unsigned long long T1i, unsigned long long T2i, double& lo, double& hi) const {
-    const double s = (double)((2.0f * cand_t(mx, c, n)) / denf);
+    bounds_s((double)((2.0f * cand_t(mx, c, n)) / denf), T1i, T2i, lo, hi);
+  }
+  // the same with the candidate's scale s_c = fl(2 t_c / den) already at hand
+  __device__ void bounds_s(double s, unsigned long long T1i, unsigned long long T2i, double& lo, double& hi) const {
     const double T1 = (double)T1i * fixu;
     const double T2 = (double)T2i;
     const double A = S2 - 2.0 * s * T1 + s * s * T2;

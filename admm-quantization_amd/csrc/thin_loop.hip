@@ -83,17 +83,23 @@ struct ThinM {
   f2v xy[kTLKPairs][2], zw[kTLKPairs][2];   // [pair][k parity] columns (x, y) and (z, w)
 };
 struct ThinGeo {
-  int kp, cg, kpl, JN, LDP, kc0;
+  int kpa, kpb, cg, kpl, JN, LDP, kc0, cw;
 };
 // Reduction chunk [kc0, kc0 + 1152) of ld (factors with ld > 1152 take several: each class
 // chain continues across them in ascending k, so the order is the same as one long chain)
 constexpr int kTSChunk = 128 * kTLKPairs;
-__device__ __forceinline__ ThinGeo thin_geo(int ld, int kc0) {
+// cw = 32: thread (cg = lane >> 3, class kpa = 8 wave + (lane & 7)), k pair slots 0..8.
+// cw = 64 (persistent loop only, ld <= 512): thread (cg = lane >> 2, classes kpa = 8 wave +
+// (lane & 3) in slots 0..3 and kpb = kpa + 4 in slots 4..7): the same chains, the same tree.
+__device__ __forceinline__ ThinGeo thin_geo(int ld, int kc0, int cw = kTSCols) {
   ThinGeo g;
   const int lane = threadIdx.x & 63;
-  g.kpl = lane & 7;
-  g.cg = lane >> 3;
-  g.kp = 8 * (threadIdx.x >> 6) + g.kpl;
+  const bool w64 = cw == 64;
+  g.cw = cw;
+  g.kpl = w64 ? (lane & 3) : (lane & 7);
+  g.cg = w64 ? (lane >> 2) : (lane >> 3);
+  g.kpa = 8 * (threadIdx.x >> 6) + g.kpl;
+  g.kpb = g.kpa + 4;
   g.kc0 = kc0;
   g.JN = (min(ld - kc0, kTSChunk) + 127) >> 7;   // k pairs per class in this chunk (<= kTLKPairs)
   g.LDP = 128 * g.JN;                               // staged row length of P (zero tail)
@@ -103,54 +109,73 @@ __device__ __forceinline__ ThinGeo thin_geo(int ld, int kc0) {
 // prepare launches)
 __device__ __forceinline__ void thin_load_m(const ProbDesc& p, int col0, const ThinGeo& g, ThinM& m) {
   const int ld = p.ld, ldm = p.ldm, cth = col0 + 4 * g.cg;
+  const bool w64 = g.cw == 64;
 #pragma unroll
   for (int j = 0; j < kTLKPairs; ++j)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int k = g.kc0 + 2 * (g.kp + 64 * j) + e;
+      const int cls = (w64 && j >= 4) ? g.kpb : g.kpa;
+      const int jj = (w64 && j >= 4) ? j - 4 : j;
+      const int k = g.kc0 + 2 * (cls + 64 * jj) + e;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j < g.JN && k < ld) v = gld4(p.M + (size_t)k * ldm + cth);
+      if (jj < g.JN && k < ld && !(w64 && j >= 8)) v = gld4(p.M + (size_t)k * ldm + cth);
       m.xy[j][e] = f2v{v.x, v.y};
       m.zw[j][e] = f2v{v.z, v.w};
     }
 }
 // P rows [0, NR) into Ps[NR][kTSChunk] (row stride fixed so every LDS read of the FMA
-// sweep is one base register plus an immediate offset; columns [0, LDP), zero past ld) with 16-B sc1 buffer loads: all loads
-// first, then the LDS stores. Rows I..NR-1 of the padded P are 0.
+// sweep is one base register plus an immediate offset; columns [0, LDP), zero past ld)
+// with 16-B sc1 buffer loads: all loads first (thin_load_p), then the LDS stores
+// (thin_store_p). Rows I..NR-1 of the padded P are 0.
 template <int NR>
-__device__ __forceinline__ void thin_stage_p(const ProbDesc& p, const ThinGeo& g, float* Ps) {
-  constexpr int kMaxV4 = (NR * kTSChunk / 4 + kTLThreads - 1) / kTLThreads;
+struct ThinP {
+  static constexpr int kV4 = (NR * kTSChunk / 4 + kTLThreads - 1) / kTLThreads;
+  float4 v[kV4];
+};
+template <int NR>
+__device__ __forceinline__ void thin_load_p(const ProbDesc& p, const ThinGeo& g, ThinP<NR>& pv) {
   const int ld = p.ld, q4 = g.LDP >> 2, nv4 = NR * q4;
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc(p.P, 0, (int)((size_t)p.Ip * ld * sizeof(float)), 0x00020000);
-  float4 pv[kMaxV4];
 #pragma unroll
-  for (int r = 0; r < kMaxV4; ++r) {
+  for (int r = 0; r < ThinP<NR>::kV4; ++r) {
     const int v = threadIdx.x + r * kTLThreads;
     const int i = v / q4, k4 = g.kc0 + 4 * (v - i * q4);
-    pv[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pv.v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (v < nv4 && k4 < ld) {
       const u32x4v w = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(((size_t)i * ld + k4) * 4), 0, 16);   // sc1
-      pv[r] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < kMaxV4; ++r) {
-    const int v = threadIdx.x + r * kTLThreads;
-    if (v < nv4) {
-      const int i = v / q4, k4 = 4 * (v - i * q4);
-      *reinterpret_cast<float4*>(Ps + i * kTSChunk + k4) = pv[r];
+      pv.v[r] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
     }
   }
 }
-// One chunk of the canonical class chains: acc[i] += P[i][k] M[k][cols] over this
-// thread's k pairs, ascending (Ps staged and visible).
 template <int NR>
-__device__ __forceinline__ void thin_accumulate(const float* Ps, const ThinGeo& g, const ThinM& m, f2v (&acc)[NR][2]) {
+__device__ __forceinline__ void thin_store_p(const ThinGeo& g, const ThinP<NR>& pv, float* Ps) {
+  const int q4 = g.LDP >> 2, nv4 = NR * q4;
 #pragma unroll
-  for (int j = 0; j < kTLKPairs; ++j) {
-    if (j < g.JN) {
-      const float* pr = Ps + 2 * (g.kp + 64 * j);
+  for (int r = 0; r < ThinP<NR>::kV4; ++r) {
+    const int v = threadIdx.x + r * kTLThreads;
+    if (v < nv4) {
+      const int i = v / q4, k4 = 4 * (v - i * q4);
+      *reinterpret_cast<float4*>(Ps + i * kTSChunk + k4) = pv.v[r];
+    }
+  }
+}
+template <int NR>
+__device__ __forceinline__ void thin_stage_p(const ProbDesc& p, const ThinGeo& g, float* Ps) {
+  ThinP<NR> pv;
+  thin_load_p<NR>(p, g, pv);
+  thin_store_p<NR>(g, pv, Ps);
+}
+// One chunk of the canonical class chains of class `cls` in M slots [LO, HI): acc[i] +=
+// P[i][k] M[k][cols] over the class's k pairs, ascending (Ps staged and visible).
+template <int NR, int LO, int HI>
+__device__ __forceinline__ void thin_accumulate(const float* Ps, const ThinGeo& g, const ThinM& m, int cls,
+                                                f2v (&acc)[NR][2]) {
+  const float* pr0 = Ps + 2 * cls;
+#pragma unroll
+  for (int j = LO; j < HI; ++j) {
+    if (j - LO < g.JN) {
+      const float* pr = pr0 + 128 * (j - LO);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
         const float2 pp = *reinterpret_cast<const float2*>(pr + i * kTSChunk);   // immediate offsets
@@ -163,35 +188,98 @@ __device__ __forceinline__ void thin_accumulate(const float* Ps, const ThinGeo& 
     }
   }
 }
-// The class sums -> H_T of the workgroup's 32 columns (DPP tree in the wave, then the 8
-// waves in order through `red`, which may alias the staged P: the first barrier keeps
-// every wave's reads of it before the partial stores). Returns the quad (row tid >> 3,
-// columns 4 (tid & 7) ..) to threads tid < NR * 8, zeros elsewhere.
+template <int NR>
+__device__ __forceinline__ void thin_zero(f2v (&acc)[NR][2]) {
+#pragma unroll
+  for (int i = 0; i < NR; ++i) acc[i][0] = acc[i][1] = f2v{0.f, 0.f};
+}
+// DPP sums of the class chains over lane bits 0..1 (quad) or 0..2 (8 lanes)
+template <int NR>
+__device__ __forceinline__ void thin_lane_sums(f2v (&acc)[NR][2], bool eight) {
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float x = acc[i][h].x, y = acc[i][h].y;
+      x += dppf<0xB1>(x); y += dppf<0xB1>(y);   // quad_perm [1,0,3,2]
+      x += dppf<0x4E>(x); y += dppf<0x4E>(y);   // quad_perm [2,3,0,1]
+      if (eight) { x += dppf<0x141>(x); y += dppf<0x141>(y); }   // row_half_mirror
+      acc[i][h] = f2v{x, y};
+    }
+}
+// The workgroup's class chains (one chunk already accumulated for cw = 32; both classes
+// computed here for cw = 64) -> H_T of its cw columns: the DPP tree
+// ((c0+c1)+(c2+c3))+((c4+c5)+(c6+c7)) in each wave (for cw = 64 the two quad trees are
+// added in that order through `stash`, LDS of 8 x NR x 64 floats not aliasing Ps), then
+// the 8 waves in order through `red`, which may alias the staged P (the first barrier
+// keeps every wave's reads of it before the partial stores). Returns the quad (row
+// tid / (cw/4), columns 4 (tid % (cw/4)) ..) to threads tid < NR cw / 4, zeros elsewhere.
 template <int NR>
 __device__ __forceinline__ float4 thin_reduce(f2v (&acc)[NR][2], float* red, const ThinGeo& g) {
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    acc[i][0].x = lane8_sum(acc[i][0].x);
-    acc[i][0].y = lane8_sum(acc[i][0].y);
-    acc[i][1].x = lane8_sum(acc[i][1].x);
-    acc[i][1].y = lane8_sum(acc[i][1].y);
-  }
+  thin_lane_sums<NR>(acc, true);
   __syncthreads();
-  const int wave = threadIdx.x >> 6;
+  const int wave = threadIdx.x >> 6, cw = g.cw, qpr = cw >> 2;
   if (g.kpl == 0) {
 #pragma unroll
     for (int i = 0; i < NR; ++i)
-      *reinterpret_cast<float4*>(red + (wave * NR + i) * kTSCols + 4 * g.cg) =
+      *reinterpret_cast<float4*>(red + (wave * NR + i) * cw + 4 * g.cg) =
           make_float4(acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y);
   }
   __syncthreads();
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  if ((int)threadIdx.x < NR * 8) {
-    const int qi = threadIdx.x >> 3, qq = threadIdx.x & 7;
-    t = *reinterpret_cast<const float4*>(red + qi * kTSCols + 4 * qq);
+  if ((int)threadIdx.x < NR * qpr) {
+    const int qi = threadIdx.x / qpr, qq = threadIdx.x - qi * qpr;
+    t = *reinterpret_cast<const float4*>(red + qi * cw + 4 * qq);
 #pragma unroll
     for (int w = 1; w < kTLThreads / 64; ++w) {
-      const float4 b = *reinterpret_cast<const float4*>(red + (w * NR + qi) * kTSCols + 4 * qq);
+      const float4 b = *reinterpret_cast<const float4*>(red + (w * NR + qi) * cw + 4 * qq);
+      t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+    }
+  }
+  return t;
+}
+// cw = 64: both classes of this thread (one chunk, ld <= 512), then the same reduction
+template <int NR>
+__device__ __forceinline__ float4 thin_solve64(const float* Ps, float* red, float* stash, const ThinGeo& g,
+                                               const ThinM& m) {
+  f2v acc[NR][2];
+  thin_zero<NR>(acc);
+  thin_accumulate<NR, 0, 4>(Ps, g, m, g.kpa, acc);
+  thin_lane_sums<NR>(acc, false);
+  const int wave = threadIdx.x >> 6;
+  if (g.kpl == 0) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+      *reinterpret_cast<float4*>(stash + (wave * NR + i) * 64 + 4 * g.cg) =
+          make_float4(acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y);
+  }
+  thin_zero<NR>(acc);
+  thin_accumulate<NR, 4, 8>(Ps, g, m, g.kpb, acc);
+  thin_lane_sums<NR>(acc, false);
+  if (g.kpl == 0) {   // T4(c0..c3) + T4(c4..c7): the 8-lane tree's last step (same lane's stash)
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const float4 a = *reinterpret_cast<const float4*>(stash + (wave * NR + i) * 64 + 4 * g.cg);
+      acc[i][0] = f2v{a.x + acc[i][0].x, a.y + acc[i][0].y};
+      acc[i][1] = f2v{a.z + acc[i][1].x, a.w + acc[i][1].y};
+    }
+  }
+  __syncthreads();
+  const int cw = 64, qpr = 16;
+  if (g.kpl == 0) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+      *reinterpret_cast<float4*>(red + (wave * NR + i) * cw + 4 * g.cg) =
+          make_float4(acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y);
+  }
+  __syncthreads();
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((int)threadIdx.x < NR * qpr) {
+    const int qi = threadIdx.x / qpr, qq = threadIdx.x - qi * qpr;
+    t = *reinterpret_cast<const float4*>(red + qi * cw + 4 * qq);
+#pragma unroll
+    for (int w = 1; w < kTLThreads / 64; ++w) {
+      const float4 b = *reinterpret_cast<const float4*>(red + (w * NR + qi) * cw + 4 * qq);
       t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
     }
   }
@@ -200,7 +288,7 @@ __device__ __forceinline__ float4 thin_reduce(f2v (&acc)[NR][2], float* red, con
 // floats of region A (P staging, then the partials) for a launch whose largest ld is maxld
 inline int thin_region_a(int nr, int maxld) {
   (void)maxld;
-  return std::max(nr * kTSChunk, 8 * nr * kTSCols);
+  return std::max(nr * kTSChunk, 8 * nr * 64);
 }
 
 // ---------------------------------------------------------------------------
@@ -241,12 +329,11 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_solve(const ProbDesc* __res
     }
   }
   f2v acc[NR][2];
-#pragma unroll
-  for (int i = 0; i < NR; ++i) acc[i][0] = acc[i][1] = f2v{0.f, 0.f};
+  thin_zero<NR>(acc);
   for (;;) {
     thin_stage_p<NR>(p, g, smemf);
     __syncthreads();
-    thin_accumulate<NR>(smemf, g, m, acc);
+    thin_accumulate<NR, 0, kTLKPairs>(smemf, g, m, g.kpa, acc);
     if (g.kc0 + kTSChunk >= ld) break;
     __syncthreads();   // the next chunk's staging overwrites smemf
     g = thin_geo(ld, g.kc0 + kTSChunk);
@@ -304,9 +391,26 @@ void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits,
 // ---------------------------------------------------------------------------
 // Persistent loop
 
+// Diagnostics (make TRACE=1; admmq_debug_thin_loop_trace): per workgroup, the summed
+// s_memrealtime ticks (10 ns) of each phase over the loop's iterations: {P staging, solve,
+// X and max, barrier 1 + max load, threshold table, stage-1 inserts, stage-1 sums + flush,
+// barrier 2, team bins load, suffix sums + bounds + S, stage 2, finalize, barrier 3, slot
+// reset, stop test, iterations}
+constexpr int kTLTraceMax = 1024;
+constexpr int kTLPhases = 16;
+__device__ unsigned long long g_tl_trace[kTLTraceMax][kTLPhases];
+int copy_thin_loop_trace(unsigned long long* host, int n) {
+  n = n < kTLTraceMax ? n : kTLTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl_trace), (size_t)n * kTLPhases * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? n
+             : -1;
+}
+
 // Team barrier number `target / nteam`: this thread's stores and atomics drained, the
 // workgroup joined, one lane arrives and polls (sc1 loads, s_sleep), the workgroup joins
-// again. false: the wait passed `polls` (the caller reports an internal fault).
+// again. false: the wait passed `polls` (the caller reports an internal fault). (Polling
+// from every wave's lane 0 with staggered starts was slower: 1.7 -> 2.1 us per barrier.)
 __device__ __forceinline__ bool team_barrier(unsigned* bar, unsigned target, unsigned polls, int* s_ok) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -359,7 +463,8 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   __shared__ unsigned long long s_mx;
   __shared__ int s_ok;
   __shared__ int s_cstar;
-  __shared__ __attribute__((aligned(16))) float s_x[NR * kTSCols];   // the workgroup's X (rows < NR)
+  __shared__ __attribute__((aligned(16))) float s_x[NR * 64];   // the workgroup's X (rows < NR, cw columns)
+  __shared__ float s_sc[kTLMaxCand];   // this iteration's candidate scales s_c = fl(2 t_c / den)
 
   const ThinLoopUnit un = units[blockIdx.x];
   const int job = __builtin_amdgcn_readfirstlane(un.job);
@@ -367,12 +472,13 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   ThinSync& sy = syncs[job];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ld = p.ld, I = p.I, R = p.R;
-  const int col0 = un.col0, nteam = un.nteam;
+  const int col0 = un.col0, nteam = un.nteam, cw = un.cw, qpr = cw >> 2;
   const bool leader = un.rank == 0;
   const float rho = p.rho[0];
   const int n = ncand;
-  const ThinGeo g = thin_geo(ld, 0);   // ld <= 1152: one chunk (the host checks)
+  const ThinGeo g = thin_geo(ld, 0, cw);   // ld <= 1152 (cw = 64: ld <= 512): one chunk (the host checks)
   float* const Ps = reinterpret_cast<float*>(smem);
+  float* const stash = Ps + NR * kTSChunk;   // cw = 64: the first class's quad trees
   float* const thr = reinterpret_cast<float*>(smem + (size_t)region_a * 4);
   unsigned long long* const h1 = reinterpret_cast<unsigned long long*>(smem + tl_off_h1(region_a, QMAX, n));
   unsigned* const h2 = reinterpret_cast<unsigned*>(smem + tl_off_h2(region_a, QMAX, n));
@@ -382,8 +488,8 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   ThinM m;
   thin_load_m(p, col0, g, m);
   // owned quad: row qi, columns col0 + 4 qq .. + 3 (rows >= I are never owned)
-  const int qi = tid >> 3, qq = tid & 7;
-  const bool owner = tid < NR * 8 && qi < I;
+  const int qi = tid / qpr, qq = tid - qi * qpr;
+  const bool owner = tid < NR * qpr && qi < I;
   const int qcol = col0 + 4 * qq, qoff = qi * ld + qcol;
   float4 h4 = make_float4(0.f, 0.f, 0.f, 0.f), u4 = h4, f4 = h4;
   if (owner) { h4 = gld4(p.H + qoff); u4 = gld4(p.U + qoff); f4 = gld4(p.Fp + qoff); }
@@ -392,10 +498,38 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
 
   unsigned nbar = 0;
   bool fault = false;
+  unsigned long long ph[kTLPhases] = {}, tph = ADMMQ_NOW();
+#define ADMMQ_TL_PH(k)                                   \
+  if (ADMMQ_TRACE) {                                     \
+    const unsigned long long tn_ = ADMMQ_NOW();          \
+    ph[k] += tn_ - tph;                                  \
+    tph = tn_;                                           \
+  }
   for (int it = 0; it < n_iter; ++it) {
     const int slot = it & 1;
+    if (ADMMQ_TRACE) ph[15] += 1;
+    // the next P's loads, then the stop test's residual sums (previous iteration, team
+    // totals): the test is decided after the solve, so the load's latency hides behind it;
+    // nothing of this iteration is stored before the test
+    ThinP<NR> pv;
+    thin_load_p<NR>(p, g, pv);
+    const double rsum = (it > 0 && tid < 4) ? ald_f64(&sy.res[slot ^ 1][tid]) : 0.0;
+    // ---- solve
+    thin_store_p<NR>(g, pv, Ps);
+    __syncthreads();
+    ADMMQ_TL_PH(0);
+    float4 t4;
+    if (cw == 64) {
+      t4 = thin_solve64<NR>(Ps, Ps, stash, g, m);
+    } else {
+      f2v acc[NR][2];
+      thin_zero<NR>(acc);
+      thin_accumulate<NR, 0, kTLKPairs>(Ps, g, m, g.kpa, acc);
+      t4 = thin_reduce<NR>(acc, Ps, g);
+    }
+    ADMMQ_TL_PH(1);
     if (it > 0) {   // stop test on the previous iteration's team sums (source/admm.py:62-65)
-      if (tid < 4) s_res[tid] = ald_f64(&sy.res[slot ^ 1][tid]);
+      if (tid < 4) s_res[tid] = rsum;
       __syncthreads();
       const double t0 = s_res[0], t1 = s_res[1], t2 = s_res[2], t3 = s_res[3];
       if (t0 / t1 < (double)eps && t2 / t3 < (double)eps) {
@@ -403,14 +537,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
         break;
       }
     }
-    // ---- solve
-    thin_stage_p<NR>(p, g, Ps);
-    __syncthreads();
-    f2v acc[NR][2];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) acc[i][0] = acc[i][1] = f2v{0.f, 0.f};
-    thin_accumulate<NR>(Ps, g, m, acc);
-    const float4 t4 = thin_reduce<NR>(acc, Ps, g);
+    ADMMQ_TL_PH(14);
     float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned amax = 0u;
     if (owner) {
@@ -422,7 +549,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       *(gst4t*)(p.HT + qoff) = gf32x4{t4.x, t4.y, t4.z, t4.w};   // read after the launch only
       if (p.X_dbg) *(gst4t*)(p.X + qoff) = gf32x4{x4.x, x4.y, x4.z, x4.w};
     }
-    if (tid < NR * 8) *reinterpret_cast<float4*>(s_x + 4 * tid) = x4;   // rows >= I: 0
+    if (tid < NR * qpr) *reinterpret_cast<float4*>(s_x + 4 * tid) = x4;   // rows >= I: 0
     amax = wave_max_u32(amax);
     if (lane == 0) s_amax[wave] = amax;
     __syncthreads();
@@ -433,18 +560,32 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       if (mm) atomicMax(&sy.mx[slot], (unsigned long long)mm);
     }
     // ---- barrier 1: the team's max |X|
+    ADMMQ_TL_PH(2);
     if (!team_barrier(&sy.bar, nteam * ++nbar, wait_polls, &s_ok)) { fault = true; break; }
     if (tid == 0) s_mx = ald_u64(&sy.mx[slot]);
     __syncthreads();
+    ADMMQ_TL_PH(3);
     const float mx = __uint_as_float((unsigned)s_mx);
     QParams qp;
     if (mse_degenerate(mx)) {
       qp = qparams_mse(bits, __builtin_nanf(""));
     } else {
       // ---- stage 1 over the workgroup's elements, one per thread
-      fill_thresholds(thr, mx, n, QMAX, kTLThreads);
+      {   // thr[k-1][c] = fill_thresholds' values; thread (c, half of the levels): s_c computed once
+        constexpr int KH = (QMAX + 1) / 2;
+        const float den = (float)(2 * QMAX - 1);
+        for (int e = tid; e < 2 * n; e += kTLThreads) {
+          const int c = e >> 1, k0 = 1 + (e & 1) * KH;
+          const float sc = (2.0f * cand_t(mx, c, n)) / den;
+          if (!(e & 1)) s_sc[c] = sc;
+#pragma unroll
+          for (int k = k0; k < k0 + KH; ++k)
+            if (k <= QMAX) thr[(k - 1) * n + c] = level_threshold_fast(sc, k);
+        }
+      }
       for (int b = tid; b < n + 65; b += kTLThreads) { h1[b] = 0ull; h2[b] = 0u; }
       __syncthreads();
+      ADMMQ_TL_PH(4);
       const float S0 = (float)(0.2 * (double)mx);
       const float E0 = (float)(1.2 * (double)mx);
       const float inv_step = (float)(n - 1) / (E0 - S0);
@@ -456,11 +597,12 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
         float tlo0[QMAX], thin[QMAX];
 #pragma unroll
         for (int k = 0; k < QMAX; ++k) { tlo0[k] = thr[k * n]; thin[k] = thr[k * n + n - 1]; }
-        const int ne = min(I, NR) * kTSCols;   // rows >= I and columns >= R hold 0: they add nothing
-        if (tid < ne)
-          hist_insert_elem<QMAX>(s_x[tid], thr, n, S0, inv_step, K1, n + 1 + lane, tlo0, thin, h1, h2, s2, full1,
+        const int ne = min(I, NR) * cw;   // rows >= I and columns >= R hold 0: they add nothing
+        for (int e = tid; e < ne; e += kTLThreads)   // cw = 64: up to 1024 elements
+          hist_insert_elem<QMAX>(s_x[e], thr, n, S0, inv_step, K1, n + 1 + lane, tlo0, thin, h1, h2, s2, full1,
                                  full2);
       }
+      ADMMQ_TL_PH(5);
       s2 = wave_sum_f64(s2);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
@@ -484,10 +626,13 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
         if (t != 0.0) atomicAdd(&sy.s2[slot], t);
       }
       // ---- barrier 2: the team's stage-1 totals
+      ADMMQ_TL_PH(6);
       if (!team_barrier(&sy.bar, nteam * ++nbar, wait_polls, &s_ok)) { fault = true; break; }
+      ADMMQ_TL_PH(7);
       for (int b = tid; b <= n; b += kTLThreads) { H1[b] = ald_u64(&sy.h1[slot][b]); H2[b] = ald_u64(&sy.h2[slot][b]); }
       const double S2 = ald_f64(&sy.s2[slot]);
       __syncthreads();
+      ADMMQ_TL_PH(8);
       // T(c) = sum_{b > c} H[b]: block suffix sums of H[c + 1] (thread c)
       const unsigned long long v1 = (tid < n) ? H1[tid + 1] : 0ull, v2 = (tid < n) ? H2[tid + 1] : 0ull;
       const unsigned long long q1 = wave_suffix_u64(v1), q2 = wave_suffix_u64(v2);
@@ -506,7 +651,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       cx.Nterm = (double)((long long)p.mv.nelem * QMAX);
       cx.tiny = 8.0 * (double)p.mv.nelem * 0x1p-149;
       double lo = 1e300, hi = 1e300;
-      if (tid < n) cx.bounds(tid, T1, T2, lo, hi);
+      if (tid < n) cx.bounds_s((double)s_sc[tid], T1, T2, lo, hi);
       const double wm = wave_min_f64(hi);
       if (lane == 0) s_wmin[wave] = wm;
       __syncthreads();
@@ -525,20 +670,21 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       const bool all = total > kMaxSel || total == 0;
       const int ns = all ? n : total;
       int cstar;
+      ADMMQ_TL_PH(9);
       if (ns == 1) {
         cstar = lsel[2];
       } else {
         // ---- stage 2 (rare): the canonical SSE of S over the team (oracle/quant_oracle.py)
         const int K = fixed_exp(mx, p.nq);
         const int q = 1 << (bits - 1);
-        const float qlo = (float)(-q), qhi = (float)(q - 1), den = (float)(2 * q - 1);
+        const float qlo = (float)(-q), qhi = (float)(q - 1);
         for (int j = tid; j < ns; j += kTLThreads) s_part[j] = 0ull;
         __syncthreads();
         for (int j = 0; j < ns; ++j) {
           const int c = all ? j : lsel[2 + j];
           unsigned long long gq = 0ull;
           if (owner) {
-            const float s = (2.0f * cand_t(mx, c, n)) / den;
+            const float s = s_sc[c];
             const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
             float dd[4];
 #pragma unroll
@@ -585,6 +731,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       qp = qparams_mse(bits, cand_t(mx, cstar, n));
     }
     // ---- finalize (admm_finalize_block's float32 operations, in the same order)
+    ADMMQ_TL_PH(10);
     double r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0;
     if (owner) {
       const float ts[4] = {t4.x, t4.y, t4.z, t4.w}, xs[4] = {x4.x, x4.y, x4.z, x4.w};
@@ -621,7 +768,9 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
     }
     if (leader && tid == 0) p.flags[1] = it + 1;
     // ---- barrier 3: the next P and the residual sums
+    ADMMQ_TL_PH(11);
     if (!team_barrier(&sy.bar, nteam * ++nbar, wait_polls, &s_ok)) { fault = true; break; }
+    ADMMQ_TL_PH(12);
     if (leader) {   // every reader of this slot (and of the other slot's residuals) is past it
       for (int b = tid; b <= n; b += kTLThreads) {
         ast_u64(&sy.h1[slot][b], 0ull);
@@ -631,7 +780,11 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       if (tid == 0) { ast_u64(&sy.mx[slot], 0ull); ast_f64(&sy.s2[slot], 0.0); }
       if (tid < 4) ast_f64(&sy.res[slot ^ 1][tid], 0.0);
     }
+    ADMMQ_TL_PH(13);
   }
+#undef ADMMQ_TL_PH
+  if (ADMMQ_TRACE && tid == 0 && blockIdx.x < kTLTraceMax)
+    for (int k = 0; k < kTLPhases; ++k) g_tl_trace[blockIdx.x][k] = ph[k];
   if (fault) {
     if (tid == 0) p.flags[3] = 1;   // internal fault: the caller re-runs without this loop
     return;
@@ -647,7 +800,7 @@ int launch_thin_loop(const ProbDesc* d, const ThinLoopUnit* units, int nunits, T
   if (nunits <= 0 || nunits > ncu || n_iter <= 0 || maxld > 1152) return -1;
   if (ncand < 2 || ncand > kTLMaxCand || bits < 2 || bits > 5) return -1;
   const int NRv = nr <= 9 ? 9 : 16;
-  const int region_a = thin_region_a(NRv, maxld);
+  const int region_a = NRv * kTSChunk + 8 * NRv * 64;   // staged P / partials, then the cw = 64 stash
   const size_t lds = thin_loop_lds_bytes(region_a, ncand, bits);
   if (lds > 160 * 1024 - 12 * 1024) return -1;   // leaves room for the static LDS
   auto run = [&](auto kern) -> int {

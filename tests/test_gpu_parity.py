@@ -435,7 +435,7 @@ def test_thin_loop_equals_per_iteration(torch_dev, eps, bits, na):
     iteration in one persistent launch (k_thin_loop: M in registers, team barriers). It
     gives the bits of the per-iteration launches (k_thin_solve + k_mse_small_admm): H, U
     and the iteration counts (eps = 1e-3 exercises the team's stop test), with no internal
-    fault; 2..5 bits and 64..256 candidates."""
+    fault; 2..5 bits and 64..256 candidates; 32- and 64-column workgroups."""
     torch, dev = torch_dev
     from admmq import admm_iteration_batched, _lib
     probs_np = [_layer_problem(l, 2) for l in ("layer1.0.conv1", "layer2.1.conv1", "layer3.1.conv2", "layer4.1.conv2",
@@ -448,14 +448,17 @@ def test_thin_loop_equals_per_iteration(torch_dev, eps, bits, na):
             Hs, info = admm_iteration_batched(ps, 12, eps, bits, MSE, num_attempts=na, return_info=True)
         return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
 
-    a, ia = run(True)
     b, ib = run(False)
-    assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
-    assert np.array_equal(ia, ib), (ia, ib)
-    for (ha, ua), (hb, ub) in zip(a, b):
-        assert _bits_equal(ha, hb) and _bits_equal(ua, ub)
+    # 32-column teams, then 64-column workgroups wherever ld <= 512 (two k classes per
+    # thread: the same chains and the same sum tree)
+    for mode in (True, "wide"):
+        a, ia = run(mode)
+        assert (ia[:, 3] == 0).all() and (ib[:, 3] == 0).all()
+        assert np.array_equal(ia, ib), (mode, ia, ib)
+        for (ha, ua), (hb, ub) in zip(a, b):
+            assert _bits_equal(ha, hb) and _bits_equal(ua, ub), mode
     if eps == 0.0:
-        assert (ia[:, 0] == 11).all()
+        assert (ib[:, 0] == 11).all()
 
 
 def test_thin_loop_one_step_vs_oracle(torch_dev):

@@ -154,7 +154,7 @@ SPLIT_PRODUCTS = 3             # split-fp16 solve: Ph Mh + Ph Ml + Pl Mh per sol
 #                     call: M, F, H, U, P in, H, U out: 4 (R^2 + 6 I R) B
 PROF_CLASSES = ["gemm", "gemm_thin", "search", "small", "finalize", "prepare", "thin_loop"]
 PER_ITER_CLASSES = PROF_CLASSES[:5]
-KERNEL_NAMES = {"gemm": "k_gemm (solve, split-f16 MFMA)", "gemm_thin": "k_thin_solve (solve, I<=16, VALU)",
+KERNEL_NAMES = {"gemm": "k_gemm (solve GEMM)", "gemm_thin": "k_thin_solve (solve, I<=16, VALU)",
                 "search": "k_mse_hist3 (two-stage MSE search)", "small": "k_mse_small_admm (I<=16 search+finalize)",
                 "finalize": "k_finalize_admm (projection + dual update)", "prepare": "prepare (rho, SPD inverse, planes)",
                 "thin_loop": "k_thin_loop (persistent: every iteration of the I<=16 factors, VALU solve)"}
@@ -223,6 +223,7 @@ def kernel_roofline(cls, work_tuple, avg_us, launches, split, traffic):
               "launch_avg_us": avg_us, "launches_timed": launches, "algorithmic_bytes_per_launch": by,
               "algorithmic_flops_per_launch": fl, "t_ideal_us": max(t_mfma, t_hbm) * 1e6})
     if cls == "gemm":
+        r["kernel"] = "k_gemm (solve, split-f16 MFMA)" if split else "k_gemm (solve, fp32 MFMA)"
         r["mfma_form"] = "split-f16 (v_mfma_f32_32x32x16_f16, 3 products)" if split else "fp32 (v_mfma_f32_32x32x2_f32)"
     if ve:
         r["valu_equiv"] = {"achieved": ve / t / 1e12, "peak": PEAK_F32, "unit": "TFLOP/s",

@@ -324,11 +324,12 @@ static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
 // the tiles at positions b, b + ncu, b + 2 ncu share one CU's MFMA pipes. Longest-first
 // order alone gives some CUs three long tiles and others two; instead every tile, longest
 // first, goes to the CU with the fewest K-steps that still has a free slot.
+// The grid is padded with empty tiles (nk = 0: the workgroup returns at once) to a whole
+// number of rounds, so every CU may take up to `slots` tiles, not only the CUs whose
+// positions exist in a partial last round (C3 mode 1: 645 tiles, max CU load 90 -> 84).
 static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots) {
   const int n = (int)tiles.size();
   if (n <= ncu || n > ncu * slots) return;
-  const int rounds = (n + ncu - 1) / ncu;
-  const int full = n - (rounds - 1) * ncu;   // CUs 0 .. full-1 take `rounds` tiles, the rest one fewer
   std::vector<GemmTile> sorted = tiles;
   auto cost = [](const GemmTile& t) { return (long long)t.nk * ((t.bm > 0 ? t.bm : 64) / 32); };   // 32-row K-steps
   std::stable_sort(sorted.begin(), sorted.end(), [&](const GemmTile& a, const GemmTile& b) { return cost(a) > cost(b); });
@@ -345,8 +346,7 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
     int best = -1;
     long long best_key = 0;
     for (int b = 0; b < ncu; ++b) {
-      const int cap = b < full ? rounds : rounds - 1;
-      if ((int)bins[b].size() >= cap) continue;
+      if ((int)bins[b].size() >= slots) continue;
       // smaller is better: load first, then affinity (column, row)
       const long long key = load[b] * 1000000LL - cx[b % kXcd] * 1000LL - rx[b % kXcd];
       if (best < 0 || key < best_key) { best = b; best_key = key; }
@@ -356,6 +356,10 @@ static void order_tiles_for_cus(std::vector<GemmTile>& tiles, int ncu, int slots
     cx[best % kXcd] += 1;
     rx[best % kXcd] += 1;
   }
+  size_t rounds = 0;
+  for (int b = 0; b < ncu; ++b) rounds = std::max(rounds, bins[b].size());
+  GemmTile empty = mk_tile(0, 0, 0, 0, 0);
+  tiles.assign(rounds * ncu, empty);
   for (int b = 0; b < ncu; ++b)
     for (int r = 0; r < (int)bins[b].size(); ++r) tiles[b + (size_t)r * ncu] = bins[b][r];
 }
@@ -846,6 +850,12 @@ using namespace admmq;
 static int valid_scheme(int q) { return q >= 0 && q <= 3; }
 static int valid_bits(int b) { return b >= 1 && b <= 16; }
 
+static const int g_gemm_stage_env = [] {
+  const char* e = std::getenv("ADMMQ_GEMM_F32_STAGE");
+  if (e && *e >= '0' && *e <= '3' && e[1] == 0) g_gemm_f32_stage = *e - '0';
+  return 0;
+}();
+
 extern "C" {
 
 int32_t admmq_version(void) { return 100; }
@@ -913,6 +923,17 @@ int32_t admmq_debug_set_fin_wait_polls(uint32_t polls) {
 int32_t admmq_debug_set_gemm_ks(int32_t ks) {
   if (ks != 1 && ks != 2) return fail(ADMMQ_ERR_ARG, "ks must be 1 or 2");
   g_gemm_ks_f32 = ks;
+  return ADMMQ_OK;
+}
+
+// diagnostics (not in include/admmq.h): staging form of the fp32 64 x 64 tiles (same bits):
+// 0 = k_gemm's global_load_lds with per-lane 64-bit addresses, 1 = k_gemm_f32b (buffer
+// loads with a scalar K offset, U prefetched), 2 = k_gemm_f32b with a 2-deep
+// ring, 3 = k_gemm_f32b without the U prefetch (the default: C3 mode 0 0.655 -> 0.597 us per
+// 64x64 K-step per CU against 0). ADMMQ_GEMM_F32_STAGE sets it at load time.
+int32_t admmq_debug_set_gemm_stage(int32_t v) {
+  if (v < 0 || v > 3) return fail(ADMMQ_ERR_ARG, "stage must be 0..3");
+  g_gemm_f32_stage = v;
   return ADMMQ_OK;
 }
 

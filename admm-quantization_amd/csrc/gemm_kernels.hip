@@ -154,6 +154,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
   const unsigned long long T0 = ADMMQ_NOW();
   const unsigned long long C0 = ADMMQ_TRACE ? __builtin_amdgcn_s_memtime() : 0ull;
   const GemmTile tl = tiles[blockIdx.x];
+  if (tl.nk <= 0) return;   // grid padding (order_tiles_for_cus)
   const ProbDesc& p = probs[tl.prob];
   const int ld = tl.ld, ldm = tl.ldm;
   const int row0 = tl.tm * BM, col0 = tl.tn * BNT;
@@ -588,6 +589,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   float* const stp[4] = {st0, st1, st2, st3};
   __shared__ unsigned red[3][4];
   const GemmTile tl = tiles[blockIdx.x];
+  if (tl.nk <= 0) return;   // grid padding (order_tiles_for_cus)
   if (tl.bm == 128) f32_tile<128, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
   else if (tl.bm == 64) f32_tile<64, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
   else f32_tile<32, NS>(probs, tl, slot, iter, eps, ncand, stp, red);
@@ -604,6 +606,180 @@ void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_
   if (nslots > 0)
     hipLaunchKernelGGL(k_gemm_f32p<3>, dim3(nslots), dim3(256), 0, s, d, tiles, list_off, slot, iter, eps, ncand);
 }
+
+// ---------------------------------------------------------------------------
+// fp32 64 x 64 tiles with scalar-offset staging (kSolveF32, the C3 / C4 launches): the
+// same tile, wave layout, K order and epilogue as k_gemm<2, 1, NS, false> (identical
+// bits), but the global -> LDS pieces are buffer_load ... lds with a per-lane offset fixed
+// for the whole tile and the K-step's byte offset in an SGPR, and the pieces' LDS bases
+// (M0) are wave-uniform scalars: the K-loop issues no VALU address arithmetic (the fp32
+// MFMA runs on the same SIMD pipe as the VALU, so every VALU instruction in the loop
+// costs MFMA time; tools/probes/mix_probe.hip). The buffer descriptors are rebased per
+// tile (P at the tile's first row, M at its first column's row), so every offset stays
+// far below 2^31 whatever the problem size. PRE: the epilogue's U entries are loaded
+// before the K-loop (their latency hidden, 16 more VGPRs).
+typedef __attribute__((address_space(3))) void lds_void;
+template <int NS, bool PRE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4 : 3))) void k_gemm_f32b(
+    const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
+  constexpr int BM = 64, ROWS = 128, STAGE = ROWS * 32, GPW = 4;
+  __shared__ __attribute__((aligned(16))) float st0[STAGE];
+  __shared__ __attribute__((aligned(16))) float st1[STAGE];
+  __shared__ __attribute__((aligned(16))) float st2[NS > 2 ? STAGE : 4];
+  float* const stp[3] = {st0, st1, st2};
+  __shared__ unsigned red[3][4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: the LDS bases below stay in SGPRs
+  const int wm = wave >> 1, wn = wave & 1;
+  const int i = lane & 31, h = lane >> 5;
+  const int swz = (i >> 1) & 7;
+  const int aoff = (32 * wm + i) * 32, boff = (BM + 32 * wn + i) * 32;
+  const unsigned long long T0 = ADMMQ_NOW();
+  const unsigned long long C0 = ADMMQ_TRACE ? __builtin_amdgcn_s_memtime() : 0ull;
+  const GemmTile tl = tiles[blockIdx.x];
+  if (tl.nk <= 0) return;   // grid padding (order_tiles_for_cus)
+  const ProbDesc& p = probs[tl.prob];
+  const int ld = tl.ld, ldm = tl.ldm;
+  const int row0 = tl.tm * BM, col0 = tl.tn * 64;
+  const int nk = tl.nk;
+  float upre[16];
+  auto load_u = [&]() {
+    const int col = col0 + 32 * wn + i;
+    const int colc = col < ld ? col : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      upre[r] = ldg(tl.U + (size_t)row * ld + colc);
+    }
+  };
+  if constexpr (PRE) load_u();
+  // waves 0, 1 stage the 64 P rows (image rows 0..63), waves 2, 3 the 64 M rows
+  const bool isA = wave < 2;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      isA ? (void*)(tl.P + (size_t)row0 * ld) : (void*)(tl.M + (size_t)col0 * ldm), 0, 0x7FFFFFFF, 0x00020000);
+  unsigned voff[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int r = 8 * (wave * GPW + j) + (lane >> 3);        // image row
+    const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
+    voff[j] = isA ? (unsigned)((r * ld + 4 * c) * 4) : (unsigned)((min(r - BM, ldm - 1 - col0) * ldm + 4 * c) * 4);
+  }
+#define ADMMQ_ISSUE(s, kt)                                                                            \
+  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                                                    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(stp[s] + (wave * GPW + j) * 256), 16, voff[j], \
+                                             (kt) * (BK * 4), 0, 0)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
+  bool skip = p.flags[0] != 0;
+  if (!skip && converged_before(p, slot ^ 1, iter, eps)) {
+    if (tl.first && tid == 0) p.flags[0] = 1;   // sticky "break" (source/admm.py:64-65)
+    skip = true;
+  }
+  if (skip) {
+    wait_vmcnt<0>();
+    return;
+  }
+  if (tl.first) {   // this iteration's quantizer-search accumulators start at zero
+    unsigned long long* sse = p.mv.sse + (size_t)slot * ncand;
+    unsigned long long* h1 = p.mv.h1 + (size_t)slot * kHistRep * (ncand + 1);
+    unsigned long long* h2 = p.mv.h2 + (size_t)slot * kHistRep * (ncand + 1);
+    for (int c = tid; c < ncand; c += 256) sse[c] = 0ull;
+    for (int c = tid; c < kHistRep * (ncand + 1); c += 256) { h1[c] = 0ull; h2[c] = 0ull; }
+    if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#define ADMMQ_STEP(s, kt)                                                                     \
+  do {                                                                                        \
+    wait_vmcnt<GPW * (NS - 2)>();                                                             \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
+    raw_barrier();                                                                            \
+    ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
+    const float* st = stp[s];                                                                 \
+    float4 fa[2], fb[2];                                                                      \
+    _Pragma("unroll") for (int qq = 0; qq < 4; ++qq) {                                        \
+      if (qq == 0) {                                                                          \
+        const int cp = ((4 * h) ^ swz) * 4;                                                   \
+        fa[0] = *reinterpret_cast<const float4*>(st + aoff + cp);                             \
+        fb[0] = *reinterpret_cast<const float4*>(st + boff + cp);                             \
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                                    \
+      }                                                                                       \
+      if (qq + 1 < 4) {                                                                       \
+        const int cn = ((4 * h + qq + 1) ^ swz) * 4;                                          \
+        fa[(qq + 1) & 1] = *reinterpret_cast<const float4*>(st + aoff + cn);                  \
+        fb[(qq + 1) & 1] = *reinterpret_cast<const float4*>(st + boff + cn);                  \
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                                    \
+      }                                                                                       \
+      const float4 a = fa[qq & 1], b = fb[qq & 1];                                            \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);                     \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);                     \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);                     \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);                     \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                      \
+    }                                                                                         \
+  } while (0)
+  const int nfull = nk / NS * NS;
+  for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ADMMQ_STEP(s, kt0 + s);
+  }
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (nfull + s < nk) ADMMQ_STEP(s, nfull + s);
+#undef ADMMQ_STEP
+#undef ADMMQ_ISSUE
+  wait_vmcnt<0>();   // the refills past the end land before the workgroup ends
+  if constexpr (!PRE) load_u();
+  unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+  typedef __attribute__((address_space(1))) float gf32;
+  gf32* const HTg = (gf32*)p.HT;
+  gf32* const Xg = p.X_dbg ? (gf32*)p.X : nullptr;   // debug output only
+  const int pI = p.I, pR = p.R;
+  const int col = col0 + 32 * wn + i;
+  if (col < ld) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const size_t off = (size_t)row * ld + col;
+      const float ht = acc[r];
+      const float x = ht - upre[r];
+      HTg[off] = ht;
+      if (Xg) Xg[off] = x;
+      if (row < pI && col < pR) {
+        amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);
+        const unsigned e = enc_ord(x);
+        mn = min(mn, e);
+        mxo = max(mxo, e);
+      }
+    }
+  }
+  amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
+  if (lane == 0) { red[0][wave] = amax; red[1][wave] = mn; red[2][wave] = mxo; }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned a0 = red[0][0], a1 = red[1][0], a2 = red[2][0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) { a0 = max(a0, red[0][w]); a1 = min(a1, red[1][w]); a2 = max(a2, red[2][w]); }
+    unsigned* stt = p.mv.stat + 4 * slot;
+    atomicMax(&stt[0], a0);
+    atomicMin(&stt[1], a1);
+    atomicMax(&stt[2], a2);
+    if (ADMMQ_TRACE && blockIdx.x < kGemmTraceMax) {
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+      g_gemm_trace[blockIdx.x][0] = T0;
+      g_gemm_trace[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - C0;
+      g_gemm_trace[blockIdx.x][1] = ADMMQ_NOW();
+      g_gemm_trace[blockIdx.x][2] = ((unsigned long long)blockIdx.x << 48) | ((unsigned long long)(nk & 0xFF) << 40) |
+                                    ((unsigned long long)(xcc & 0xFF) << 32) | hw;
+    }
+  }
+}
+
+// fp32 64 x 64 tiles: 0 = k_gemm<2, 1, 3, false>, 1 = k_gemm_f32b<3, true>, 2 = k_gemm_f32b<2, false>,
+// 3 = k_gemm_f32b<3, false> (same bits)
+int g_gemm_f32_stage = 3;
 
 // One block per (problem, row): rows [0, Ip) of P (fp32, padded, zero pads) -> P2 / eP.
 // `which` 0: P of every split problem; 1: M (rows [0, ldm)) -> M2 / eM.
@@ -661,6 +837,15 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
   if (ntiles_big > 0) {
     if (!split && g_gemm_ks_f32 == 2)   // 8 waves per 64 x 64 tile, each K-step split over two waves (A/B)
       hipLaunchKernelGGL((k_gemm<2, 2, 3, false>), dim3(ntiles_big), dim3(512), 0, s, d, tiles + ntiles_wide, slot, iter,
+                         eps, ncand);
+    else if (!split && g_gemm_f32_stage == 1)
+      hipLaunchKernelGGL((k_gemm_f32b<3, true>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
+                         eps, ncand);
+    else if (!split && g_gemm_f32_stage == 2)
+      hipLaunchKernelGGL((k_gemm_f32b<2, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
+                         eps, ncand);
+    else if (!split && g_gemm_f32_stage == 3)
+      hipLaunchKernelGGL((k_gemm_f32b<3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
                          eps, ncand);
     else
       ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);

@@ -107,6 +107,7 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_f32_persistent": (I32, [I32, I32]),
         "admmq_debug_set_gemm_ks": (I32, [I32]),
         "admmq_debug_set_gemm_stage": (I32, [I32]),
+        "admmq_debug_set_even_units": (I32, [I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
         "admmq_debug_set_thin_loop": (I32, [I32]),
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),

@@ -95,6 +95,7 @@ static std::atomic<int> g_f32_rule{1};
 // fp32 solve kernel: 0 = k_gemm (64 x 64 tiles), 1 = persistent tile lists (k_gemm_f32p,
 // slower: DESIGN §7), 2 = one tile per workgroup with per-problem tile rows (k_gemm_f32t)
 static std::atomic<int> g_f32_kernel{0};
+static std::atomic<int> g_even_units{1};   // big-job stage-1 units sized to fill the resident round evenly
 static int f32_tile_rows(int I, int ld) {
   if (I <= 32) return 32;
   const int rule = g_f32_rule.load();
@@ -623,6 +624,28 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   }
   pl.fin_groups = fin_groups_for(pl.desc, big_jobs.empty() ? order : big_jobs);
   pl.hist_nv = hist_units > kHistMaxUnits ? 2 : 1;   // one round of resident stage-1 blocks
+  // Stage-1 unit size of the big jobs: kHistElems x hist_nv, or smaller when that would
+  // leave the one round of resident blocks (2 per CU) partly filled: C3 mode 0 had 371
+  // units of ~8 k elements, so 115 CUs ran two blocks (16 k elements) and 141 one; units
+  // of about total / (2 x CUs) elements give every CU the same share (unit boundaries move
+  // only the order of the fp64 residual partial sums, never an element's result)
+  long long big_elems = 0;
+  for (int i : big_jobs) big_elems += (long long)pl.desc[i].I * pl.desc[i].ld;
+  long long hu_big = (long long)kHistElems * pl.hist_nv;
+  if (pl.hist_nv == 2 && g_even_units.load()) {
+    const long long slots = 2LL * device_cus();
+    int big_maxld = 0;
+    for (int i : big_jobs) big_maxld = std::max(big_maxld, pl.desc[i].ld);
+    for (long long t = std::max<long long>(big_maxld, (big_elems + slots - 1) / slots); t < hu_big; t += 256) {
+      long long units = 0;
+      for (int i : big_jobs) {
+        const ProbDesc& d = pl.desc[i];
+        const long long st = d.ld <= t ? (t / d.ld) * d.ld : t;
+        units += ((long long)d.I * d.ld + st - 1) / st;
+      }
+      if (units <= slots) { hu_big = t; break; }
+    }
+  }
   // stage-1 / finalize units of the small jobs (I <= kThinRows) go last: when their
   // fused one-block path runs (k_mse_small_admm), the launches take only the others
   pl.small.clear();
@@ -642,7 +665,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
         pl.fin_chunks.push_back({i, (int)e, d.mv.stat, d.flags, d.HT, d.U, std::min(tot, e + step), d.H, d.Fp, d.mv.sel});
       // stage-1 units: whole rows where a row fits (the fused finalize needs them), each
       // with the job's finalize inputs; `total` is the unit's end
-      const long long hu = (long long)kHistElems * pl.hist_nv;
+      const long long hu = pass == 0 ? hu_big : (long long)kHistElems * pl.hist_nv;
       const long long hstep = d.ld <= hu ? (hu / d.ld) * d.ld : hu;
       if (pass == 0 && d.ld > hu) pl.rows_aligned = false;
       int nh = 0;
@@ -853,6 +876,8 @@ static int valid_bits(int b) { return b >= 1 && b <= 16; }
 static const int g_gemm_stage_env = [] {
   const char* e = std::getenv("ADMMQ_GEMM_F32_STAGE");
   if (e && *e >= '0' && *e <= '3' && e[1] == 0) g_gemm_f32_stage = *e - '0';
+  const char* u = std::getenv("ADMMQ_EVEN_UNITS");   // diagnostics: 0 = kHistElems x nv stage-1 units
+  if (u && u[0] == '0' && u[1] == 0) g_even_units = 0;
   return 0;
 }();
 
@@ -931,6 +956,11 @@ int32_t admmq_debug_set_gemm_ks(int32_t ks) {
 // loads with a scalar K offset, U prefetched), 2 = k_gemm_f32b with a 2-deep
 // ring, 3 = k_gemm_f32b without the U prefetch (the default: C3 mode 0 0.655 -> 0.597 us per
 // 64x64 K-step per CU against 0). ADMMQ_GEMM_F32_STAGE sets it at load time.
+int32_t admmq_debug_set_even_units(int32_t on) {
+  g_even_units = on != 0;
+  return ADMMQ_OK;
+}
+
 int32_t admmq_debug_set_gemm_stage(int32_t v) {
   if (v < 0 || v > 3) return fail(ADMMQ_ERR_ARG, "stage must be 0..3");
   g_gemm_f32_stage = v;

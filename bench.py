@@ -347,6 +347,21 @@ def time_steps(work, max_iter_admm, steps, warmup):
     return 1e3 * (time.perf_counter() - t0) / steps
 
 
+def class_avgs(work, max_iter_admm, every=8):
+    """One profiled sweep: average microseconds per launch of each kernel class (HIP events
+    on the library's stream, every `every`-th iteration)."""
+    import ctypes
+    from admmq import _lib
+    lib = _lib.load()
+    _lib.check(lib.admmq_profile_begin(3 * 6 * (max_iter_admm // every + 1) + 64, every), "profile_begin")
+    run_step(work, max_iter_admm)
+    torch.cuda.synchronize()
+    ms = (ctypes.c_double * 8)()
+    cnt = (ctypes.c_int64 * 8)()
+    _lib.check(lib.admmq_profile_end(ms, cnt), "profile_end")
+    return {c: round(1e3 * ms[i] / cnt[i], 2) for i, c in enumerate(PROF_CLASSES) if cnt[i]}
+
+
 def emulate_shards(a):
     """SURVEY §8(e) readiness without a node: every rank's LPT shard of an N-GPU
     `--shard layers` run (bench.build_workload with that rank / world) is timed on this
@@ -362,16 +377,18 @@ def emulate_shards(a):
     full, _, _ = build_workload(a.model, 0, 1, "layers", device)
     full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
     del full
-    shard_ms, nlayers, info = [], [], None
+    shard_ms, nlayers, info, shard_us = [], [], None, []
     for r in range(N):
         work, _, info = build_workload(a.model, r, N, "layers", device)
         nlayers.append(len(work))
         shard_ms.append(time_steps(work, a.max_iter_admm, a.steps, a.warmup) if work else 0.0)
+        shard_us.append(class_avgs(work, a.max_iter_admm) if work else {})
         del work
         print(f"shard {r}/{N}: {nlayers[-1]} layers, {shard_ms[-1]:.1f} ms per sweep", file=sys.stderr, flush=True)
     out = {"metric": "emulated layer-shard sweep time (one GPU)", "model": a.model, "world": N, "solve": a.solve,
            "max_iter_admm": a.max_iter_admm, "steps": a.steps, "full_ms_per_sweep": full_ms,
            "shard_ms_per_sweep": shard_ms, "layers_per_rank": nlayers, "busiest_ms": max(shard_ms),
+           "shard_kernel_avg_us": shard_us,
            "implied_speedup": full_ms / max(shard_ms), "lpt_speedup_cap": info["lpt_speedup_cap"],
            "whole_layer_speedup_cap": info["whole_layer_speedup_cap"], "policy": info["policy"]}
     print(json.dumps(out), flush=True)

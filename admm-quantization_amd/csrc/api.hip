@@ -878,6 +878,8 @@ static const int g_gemm_stage_env = [] {
   if (e && *e >= '0' && *e <= '3' && e[1] == 0) g_gemm_f32_stage = *e - '0';
   const char* u = std::getenv("ADMMQ_EVEN_UNITS");   // diagnostics: 0 = kHistElems x nv stage-1 units
   if (u && u[0] == '0' && u[1] == 0) g_even_units = 0;
+  const char* fc = std::getenv("ADMMQ_FIN_CAPACITY");   // diagnostics: admmq_debug_set_fin_capacity
+  if (fc) g_fin_cap_override = std::atoi(fc);
   return 0;
 }();
 

@@ -223,7 +223,8 @@ def kernel_roofline(cls, work_tuple, avg_us, launches, split, traffic):
               "launch_avg_us": avg_us, "launches_timed": launches, "algorithmic_bytes_per_launch": by,
               "algorithmic_flops_per_launch": fl, "t_ideal_us": max(t_mfma, t_hbm) * 1e6})
     if cls == "gemm":
-        r["kernel"] = "k_gemm (solve, split-f16 MFMA)" if split else "k_gemm (solve, fp32 MFMA)"
+        r["kernel"] = ("k_gemm (solve, split-f16 MFMA)" if split
+                       else "k_gemm_f32b (solve, fp32 MFMA; 256x128 k_gemm tiles in many-round launches)")
         r["mfma_form"] = "split-f16 (v_mfma_f32_32x32x16_f16, 3 products)" if split else "fp32 (v_mfma_f32_32x32x2_f32)"
     if ve:
         r["valu_equiv"] = {"achieved": ve / t / 1e12, "peak": PEAK_F32, "unit": "TFLOP/s",

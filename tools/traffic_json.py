@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 # bench.py's launch classes (ADMMQ_PROF_*) by kernel-name prefix
-CLASSES = {"gemm": ("k_gemm<",), "gemm_thin": ("k_thin_solve",), "search": ("k_mse_hist", "k_mse_sse", "k_mse_select"),
+CLASSES = {"gemm": ("k_gemm<", "k_gemm_f32b<"), "gemm_thin": ("k_thin_solve",), "search": ("k_mse_hist", "k_mse_sse", "k_mse_select"),
            "small": ("k_mse_small_admm",), "finalize": ("k_finalize_admm",), "thin_loop": ("k_thin_loop",)}
 
 

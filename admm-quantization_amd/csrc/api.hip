@@ -192,8 +192,8 @@ static bool two_stage_ok(int ncand, int bits) {
 
 // Exact merged order of the level thresholds for (n, qmax) (k_mse_hist3): thr[k][c] is
 // within a few ulps of (2k-1) ((n-1) + 5c) times a constant, so the integer keys give
-// the order; rank0[e] for e = (k-1) n + c, and the groups of equal keys as
-// {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
+// the order; rank0[e] for e = (k-1) n + c (bit 15 set for a member of a group of equal
+// keys), and those groups as {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
 // than 4 (the per-level stage 1 is used instead).
 // rank0 is returned padded to kMaxMerged entries and followed by the coarse cell index
 // lower bound lo[g], g = 0..kCells (see h3_setup): the number of thresholds whose cell
@@ -212,7 +212,8 @@ static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, s
   for (int r = 0; r < M;) {
     int r1 = r + 1;
     while (r1 < M && key[r1].first == key[r].first) ++r1;
-    for (int j = r; j < r1; ++j) rank0[key[j].second] = (unsigned short)j;
+    // bit 15 marks a member of a tie group (its place is settled on the device, h3_setup)
+    for (int j = r; j < r1; ++j) rank0[key[j].second] = (unsigned short)(j | (r1 - r > 1 ? 0x8000 : 0));
     if (r1 - r > 1) {
       if (r1 - r > 4) return false;
       unsigned short g[6] = {(unsigned short)r, (unsigned short)(r1 - r), 0, 0, 0, 0};

@@ -202,7 +202,8 @@ void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s)
 void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits, int nr, int maxld, int slot, int iter,
                        float eps, int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
-                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s);
+                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0 = nullptr,
+                 hipEvent_t ev1 = nullptr);
 extern int g_gemm_ks_f32;
 extern int g_gemm_f32_stage;   // fp32 64 x 64 staging form (gemm_kernels.hip)
 void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
@@ -230,7 +231,7 @@ int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out)
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      unsigned wait_polls, hipStream_t s);
+                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // fused finalize: polls (s_sleep 2 each, ~10 ms in all) before a block gives up waiting for
 // its job's selection and reports an internal fault instead of finalizing
 constexpr unsigned kFinWaitPollsDefault = 1u << 17;

@@ -192,8 +192,8 @@ static bool two_stage_ok(int ncand, int bits) {
 
 // Exact merged order of the level thresholds for (n, qmax) (k_mse_hist3): thr[k][c] is
 // within a few ulps of (2k-1) ((n-1) + 5c) times a constant, so the integer keys give
-// the order; rank0[e] for e = (k-1) n + c (bit 15 set for a member of a group of equal
-// keys), and those groups as {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
+// the order; rank0[e] for e = (k-1) n + c, and the groups of equal keys as
+// {first rank, size, element indices...} padded to 6 entries. false: a tie group larger
 // than 4 (the per-level stage 1 is used instead).
 // rank0 is returned padded to kMaxMerged entries and followed by the coarse cell index
 // lower bound lo[g], g = 0..kCells (see h3_setup): the number of thresholds whose cell
@@ -212,8 +212,7 @@ static bool merged_tables(int n, int qmax, std::vector<unsigned short>& rank0, s
   for (int r = 0; r < M;) {
     int r1 = r + 1;
     while (r1 < M && key[r1].first == key[r].first) ++r1;
-    // bit 15 marks a member of a tie group (its place is settled on the device, h3_setup)
-    for (int j = r; j < r1; ++j) rank0[key[j].second] = (unsigned short)(j | (r1 - r > 1 ? 0x8000 : 0));
+    for (int j = r; j < r1; ++j) rank0[key[j].second] = (unsigned short)j;
     if (r1 - r > 1) {
       if (r1 - r > 4) return false;
       unsigned short g[6] = {(unsigned short)r, (unsigned short)(r1 - r), 0, 0, 0, 0};
@@ -237,6 +236,17 @@ static inline void prof_mark(hipStream_t s) {
 }
 static inline void prof_class(int c) {
   if (g_prof.on && g_prof.sampled && g_prof.next < g_prof.ev.size()) g_prof.cls.push_back(c);
+}
+// The event pair of one sampled launch of class c, for a launcher that has its dispatches
+// record them (hipExtLaunchKernelGGL: start of the kernel, end of the kernel), so the
+// measured time is the kernel's own, as rocprofv3 reports it, without the dispatch gap an
+// event packet between two kernels opens. Null events when not sampled.
+static inline void prof_pair(int c, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!g_prof.on || !g_prof.sampled || g_prof.next + 2 > g_prof.ev.size()) return;
+  g_prof.cls.push_back(c);
+  *e0 = g_prof.ev[g_prof.next++];
+  *e1 = g_prof.ev[g_prof.next++];
 }
 
 // Carves the workspace in a fixed order so that size and run agree exactly.
@@ -1179,16 +1189,18 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
     g_prof.sampled = it % g_prof.every == 0;
     // one event pair per launch (classes: include/admmq.h, admmq_profile_end)
     if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big + pl.nslots + pl.ntiles_f32t > 0) {
-      prof_class(ADMMQ_PROF_GEMM); prof_mark(s);
+      const bool diag = pl.nslots + pl.ntiles_f32t > 0;   // the diagnostic fp32 kernels: event packets
+      hipEvent_t g0 = nullptr, g1 = nullptr;
+      if (diag) { prof_class(ADMMQ_PROF_GEMM); prof_mark(s); } else { prof_pair(ADMMQ_PROF_GEMM, &g0, &g1); }
       if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0)
         launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
-                    num_attempts, s);
+                    num_attempts, s, g0, g1);
       if (pl.nslots > 0)
         launch_gemm_f32p(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.d_list_off, pl.nslots, slot, it, eps, num_attempts,
                          s);
       if (pl.ntiles_f32t > 0)
         launch_gemm_f32t(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.ntiles_f32t, slot, it, eps, num_attempts, s);
-      prof_mark(s);
+      if (diag) prof_mark(s);
     }
     if (!pl.thin.empty()) {
       prof_class(ADMMQ_PROF_GEMM_THIN); prof_mark(s);
@@ -1202,11 +1214,11 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
         // fused finalize: one whole-row unit per block; otherwise several units per block
         const int nh = fuse_fin ? nfin_blocks : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
         if (nh > 0) {
-          prof_class(ADMMQ_PROF_SEARCH); prof_mark(s);
+          hipEvent_t h0, h1;
+          prof_pair(ADMMQ_PROF_SEARCH, &h0, &h1);
           launch_mse_hist3(pl.d_desc, nullptr,
                            fuse_fin ? (fin_reps > 1 ? pl.d_hist_fin : pl.d_hist) : pl.d_hist_multi, nh, num_attempts,
-                           bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s);
-          prof_mark(s);
+                           bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s, h0, h1);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each
           prof_class(ADMMQ_PROF_SMALL); prof_mark(s);

@@ -36,6 +36,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "quant_device.h"
 
 // Diagnostic builds only (EXTRA=-DADMMQ_GEMM_DIAG=n, never the product library; results
@@ -816,42 +818,42 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
 int g_gemm_ks_f32 = 1;
 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
-                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s) {
+                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // tiles[0 .. ntiles_wide) are 256x128 (WM = 8, CW = 2: sixteen waves of 32 x 64, the
   // launches with many rounds of tiles), then ntiles_big 64x64 tiles (WM = 2, four
   // waves, 3-deep ring), then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors,
-  // 2 waves per sub-tile splitting each K-step, 4-deep ring)
-#define ADMMQ_GEMM(WM, KS, NS, N, T)                                                                                 \
-  do {                                                                                                               \
-    if (split)                                                                                                       \
-      hipLaunchKernelGGL((k_gemm<WM, KS, NS, true>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
-    else                                                                                                             \
-      hipLaunchKernelGGL((k_gemm<WM, KS, NS, false>), dim3(N), dim3(128 * WM * KS), 0, s, d, T, slot, iter, eps, ncand); \
-  } while (0)
+  // 2 waves per sub-tile splitting each K-step, 4-deep ring).
+  // ev0 / ev1 (profiling, may be null) are recorded by the dispatches themselves: ev0 at
+  // the start of the first launch, ev1 at the end of the last
+  const int nl = (ntiles_wide > 0) + (ntiles_big > 0) + (ntiles_small > 0);
+  int li = 0;
+  hipEvent_t a = nullptr, b = nullptr;
+  auto evs = [&]() { a = li == 0 ? ev0 : nullptr; b = li == nl - 1 ? ev1 : nullptr; ++li; };
+#define ADMMQ_LAUNCH(K, N, T, TILES) \
+  hipExtLaunchKernelGGL(K, dim3(N), dim3(T), 0, s, a, b, 0u, d, TILES, slot, iter, eps, ncand)
   if (ntiles_wide > 0) {   // 256 x 128 tiles (WM = 8, CW = 2: 16 waves of 32 x 64), three-deep ring, one workgroup per CU
-    if (split)
-      hipLaunchKernelGGL((k_gemm<8, 1, 3, true, 2>), dim3(ntiles_wide), dim3(1024), 0, s, d, tiles, slot, iter, eps, ncand);
-    else
-      hipLaunchKernelGGL((k_gemm<8, 1, 3, false, 2>), dim3(ntiles_wide), dim3(1024), 0, s, d, tiles, slot, iter, eps, ncand);
+    evs();
+    if (split) ADMMQ_LAUNCH((k_gemm<8, 1, 3, true, 2>), ntiles_wide, 1024, tiles);
+    else ADMMQ_LAUNCH((k_gemm<8, 1, 3, false, 2>), ntiles_wide, 1024, tiles);
   }
   if (ntiles_big > 0) {
-    if (!split && g_gemm_ks_f32 == 2)   // 8 waves per 64 x 64 tile, each K-step split over two waves (A/B)
-      hipLaunchKernelGGL((k_gemm<2, 2, 3, false>), dim3(ntiles_big), dim3(512), 0, s, d, tiles + ntiles_wide, slot, iter,
-                         eps, ncand);
-    else if (!split && g_gemm_f32_stage == 1)
-      hipLaunchKernelGGL((k_gemm_f32b<3, true>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
-                         eps, ncand);
-    else if (!split && g_gemm_f32_stage == 2)
-      hipLaunchKernelGGL((k_gemm_f32b<2, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
-                         eps, ncand);
-    else if (!split && g_gemm_f32_stage == 3)
-      hipLaunchKernelGGL((k_gemm_f32b<3, false>), dim3(ntiles_big), dim3(256), 0, s, d, tiles + ntiles_wide, slot, iter,
-                         eps, ncand);
-    else
-      ADMMQ_GEMM(2, 1, 3, ntiles_big, tiles + ntiles_wide);
+    evs();
+    const GemmTile* t = tiles + ntiles_wide;
+    if (split) ADMMQ_LAUNCH((k_gemm<2, 1, 3, true>), ntiles_big, 256, t);
+    else if (g_gemm_ks_f32 == 2)   // 8 waves per 64 x 64 tile, each K-step split over two waves (A/B)
+      ADMMQ_LAUNCH((k_gemm<2, 2, 3, false>), ntiles_big, 512, t);
+    else if (g_gemm_f32_stage == 1) ADMMQ_LAUNCH((k_gemm_f32b<3, true>), ntiles_big, 256, t);
+    else if (g_gemm_f32_stage == 2) ADMMQ_LAUNCH((k_gemm_f32b<2, false>), ntiles_big, 256, t);
+    else if (g_gemm_f32_stage == 3) ADMMQ_LAUNCH((k_gemm_f32b<3, false>), ntiles_big, 256, t);
+    else ADMMQ_LAUNCH((k_gemm<2, 1, 3, false>), ntiles_big, 256, t);
   }
-  if (ntiles_small > 0) ADMMQ_GEMM(1, 2, 4, ntiles_small, tiles + ntiles_wide + ntiles_big);
-#undef ADMMQ_GEMM
+  if (ntiles_small > 0) {
+    evs();
+    const GemmTile* t = tiles + ntiles_wide + ntiles_big;
+    if (split) ADMMQ_LAUNCH((k_gemm<1, 2, 4, true>), ntiles_small, 256, t);
+    else ADMMQ_LAUNCH((k_gemm<1, 2, 4, false>), ntiles_small, 256, t);
+  }
+#undef ADMMQ_LAUNCH
 }
 
 

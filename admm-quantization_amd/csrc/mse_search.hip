@@ -18,6 +18,8 @@
 #include <mutex>
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "quant_device.h"
 #include "search_device.h"
 
@@ -627,9 +629,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
   for (int c = threadIdx.x; c < n; c += nt) scand[c] = (2.0f * cand_t(mx, c, n)) / den;
   __syncthreads();
   // thresholds, each also scattered to its host-order rank (kR0 * nt >= kMaxMerged >= M);
-  // L = rank + 1. Members of exact-key tie groups (rank0 bit 15) are placed by their
-  // group's thread in the same phase, from values it computes itself (no barrier and no
-  // LDS read of thr in between: one phase less on every block's critical path)
+  // L = rank + 1 (tie groups below)
 #pragma unroll
   for (int j = 0; j < kR0; ++j) {
     const int e = threadIdx.x + j * nt;
@@ -637,14 +637,13 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
       const int k = 1 + e / n, c = e - (k - 1) * n;
       const float v = level_threshold_fast(scand[c], k);
       thr[e] = v;
-      const unsigned r0 = pre.r0v[j];
-      if (!(r0 & 0x8000u)) {
-        tsort[r0] = v;
-        rnk[e] = (unsigned short)(r0 + 1);
-      }
+      tsort[pre.r0v[j]] = v;
+      rnk[e] = (unsigned short)(pre.r0v[j] + 1);
     }
   }
   for (int i = threadIdx.x; i < nb; i += nt) { sumA[i] = 0ull; sumN[i] = 0ull; cntA[i] = 0u; cntN[i] = 0u; }
+  __syncthreads();
+  ADMMQ_SETUP_STAMP(1);
   // exact-key ties: order by actual value, L = 1 + index of the last equal value (the
   // thread's first group was prefetched; a load in the same loop would, after the join,
   // make the compiler wait for every outstanding load, the elements included)
@@ -652,11 +651,7 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
     const int r0 = gr[0], m = gr[1];
     int es[4];
     float vs[4];
-    for (int j = 0; j < m; ++j) {
-      es[j] = gr[2 + j];
-      const int k = 1 + es[j] / n, c = es[j] - (k - 1) * n;
-      vs[j] = level_threshold_fast(scand[c], k);   // = thr[es[j]] (same operation, same operands)
-    }
+    for (int j = 0; j < m; ++j) { es[j] = gr[2 + j]; vs[j] = thr[es[j]]; }
     for (int i = 1; i < m; ++i)                                 // insertion sort, stable
       for (int j = i; j > 0 && vs[j - 1] > vs[j]; --j) {
         const float tv = vs[j]; vs[j] = vs[j - 1]; vs[j - 1] = tv;
@@ -685,7 +680,6 @@ __device__ __forceinline__ float h3_setup(float mx, int n, const H3Pre& pre,
     if (j < ncw && i < kCellWords) cell32[i] = cv[j];
   }
   __syncthreads();
-  ADMMQ_SETUP_STAMP(1);
   ADMMQ_SETUP_STAMP(2);
   // the order check (sorted thresholds non-decreasing); the cell scale from the largest
   // threshold (level QMAX of the last candidate), computed directly
@@ -1406,12 +1400,13 @@ bool merged_ok(int ncand, int bits) {
 }
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      unsigned wait_polls, hipStream_t s) {
+                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   if (nchunks <= 0) return;
   const size_t lds = hist3_lds_bytes(ncand, bits);
-#define ADMMQ_H3(Q, V, F)                                                                                        \
-  hipLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, d, q, chunks, ncand, slot, \
-                     rank0, groups, ngroups, bits, iter, wait_polls)
+  // ev0 / ev1 (profiling, may be null): recorded by the dispatch itself at the kernel's start / end
+#define ADMMQ_H3(Q, V, F)                                                                                         \
+  hipExtLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, chunks, \
+                        ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
 #define ADMMQ_H3N(Q)                               \
   if (fin) {                                       \
     if (nv == 2) ADMMQ_H3(Q, 2, true);             \

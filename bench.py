@@ -409,7 +409,8 @@ def main():
                     help="inner iterations timed per (layer, mode) on the CPU (default 20; 1 for llama7b)")
     ap.add_argument("--no-profile", action="store_true", help="skip the live HIP-event kernel timing")
     ap.add_argument("--prof-every", type=int, default=16,
-                    help="HIP-event timing of one ADMM iteration in N (an event pair per launch adds a gap)")
+                    help="HIP-event timing of one ADMM iteration in N (GEMM and search: events recorded by the "
+                         "dispatch itself, the kernel's own time; the other classes: an event pair per launch)")
     ap.add_argument("--solve", choices=["split", "fp32"], default="fp32",
                     help="per-iteration solve GEMM form: fp32 MFMA (default: the reference's fp32 arithmetic) or "
                          "split-fp16 planes on f16 MFMA (opt-in, ~22-bit operands; never the headline)")

@@ -243,3 +243,40 @@ def test_c5_llama_full_layer_batch(torch_dev, mode, solve):
         assert np.array_equal(_bits(H), _bits(Hq)), name
         assert np.array_equal(_bits(U), _bits((U0n + (Hq - HT).astype(np.float32)).astype(np.float32))), name
     print(f"C5 full layer mode {mode} {solve}: worst H_T rel vs fp64 {worst:.2e}")
+
+
+def test_fp32_staging_forms_equal(torch_dev):
+    """The fp32 64x64 solve tiles have four staging forms (ADMMQ_GEMM_F32_STAGE /
+    admmq_debug_set_gemm_stage: k_gemm's global_load_lds with per-lane addresses, and
+    k_gemm_f32b's scalar-offset buffer loads with / without the U prefetch, 3- or 2-deep
+    ring). The tile, the wave layout, the K order and the epilogue are the
+    same, so every element's MFMA chain is too: H and U equal bit for bit over 3 inner
+    iterations, on factors whose launch pads the grid to whole rounds (>256 tiles) and on
+    one that fits a single round."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(5)
+
+    def prob(I, R):
+        B = torch.randn(R, 2 * R, generator=g) / (2 * R) ** 0.5
+        return (torch.randn(I, R, generator=g) * 0.1, torch.randn(I, R, generator=g), B @ B.T + 0.5 * torch.eye(R))
+
+    sets = [[prob(512, 1141), prob(256, 574), prob(128, 300)], [prob(200, 131)]]
+
+    def run(ps):
+        args = [(H.to(dev), torch.zeros(H.shape, device=dev), F.to(dev), G.to(dev)) for H, F, G in ps]
+        Hs = admm_iteration_batched(args, 4, 0.0, 4, MSE)
+        return [(h.cpu(), a[1].cpu()) for h, a in zip(Hs, args)]
+
+    try:
+        for ps in sets:
+            res = []
+            for stage in (0, 1, 2, 3):
+                _lib.check(lib.admmq_debug_set_gemm_stage(stage), "gemm_stage")
+                res.append(run(ps))
+            for r in res[1:]:
+                for (h0, u0), (h1, u1) in zip(res[0], r):
+                    assert torch.equal(h0, h1) and torch.equal(u0, u1)
+    finally:
+        _lib.check(lib.admmq_debug_set_gemm_stage(3), "gemm_stage")

@@ -68,6 +68,16 @@ __device__ __forceinline__ bool converged_before(const ProbDesc& p, int slot_pre
 // 16 B per lane global -> LDS (global_load_lds_dwordx4): LDS bytes [lds + 16 lane, +16).
 // The builtin exists only for the device pass (its LDS pointer type does not form on
 // the host, and a template kernel using it would silently lose its host launch stub).
+typedef __attribute__((address_space(3))) void lds_void;
+
+// The same from a buffer descriptor: LDS bytes [lds + 16 lane, +16) <- rs[voff + soff],
+// voff per lane, soff scalar (device pass only, like glds16)
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, float* lds, unsigned voff, unsigned soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, voff, soff, 0, 0);
+#endif
+}
+
 __device__ __forceinline__ void glds16(const float* g, float* lds) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0);
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: the LDS bases of the staging stay in SGPRs
   const int sub = wave % NSUB, ks = wave / NSUB;
   const int wm = sub / 2, wn = sub & 1;
   const int i = lane & 31, h = lane >> 5;
@@ -185,8 +195,16 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
     }
   };
   if constexpr (PRE) load_epi();
-  // per-lane global source of each of this wave's glds pieces (K-step 0)
-  const float* src[GPW];
+  // the staging pieces: buffer_load ... lds with descriptors rebased to the tile (P at its
+  // first row, M at its first column's row), a per-lane offset fixed for the tile and the
+  // K-step's byte offset in an SGPR - no VALU address arithmetic in the K-loop (the fp32
+  // MFMA shares the VALU's pipe; k_gemm_f32b). A piece is 8 image rows,
+  // all P rows or all M rows (BM is a multiple of 8), so its descriptor is wave-uniform.
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.P + (size_t)row0 * ld), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.M + (size_t)col0 * ldm), 0, 0x7FFFFFFF, 0x00020000);
+  unsigned voff[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
     const int g = wave * GPW + j;
@@ -194,12 +212,11 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
     const int c = (lane & 7) ^ ((r >> 1) & 7);               // source chunk of LDS position lane & 7
     // B rows past ldm (the last 128-column tile of a CW = 2 launch) read the last row: they
     // only feed columns >= ld, which are never stored
-    src[j] = (r < BM) ? tl.P + (size_t)(row0 + r) * ld + 4 * c
-                      : tl.M + (size_t)min(col0 + r - BM, ldm - 1) * ldm + 4 * c;
+    voff[j] = (r < BM) ? (unsigned)((r * ld + 4 * c) * 4) : (unsigned)((min(r - BM, ldm - 1 - col0) * ldm + 4 * c) * 4);
   }
-#define ADMMQ_ISSUE(s, kt)                                                 \
-  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                         \
-    glds16(src[j] + (kt) * BK, stp[s] + (wave * GPW + j) * 256)
+#define ADMMQ_ISSUE(s, kt)                                                                                      \
+  _Pragma("unroll") for (int j = 0; j < GPW; ++j)                                                              \
+    blds16(8 * (wave * GPW + j) < BM ? rsA : rsB, stp[s] + (wave * GPW + j) * 256, voff[j], (kt) * (BK * 4))
   // the first NS-1 stages go out before the stop test, whose inputs (flag, residual
   // sums) are one dependent read further away; a stopped problem drains them unused
 #pragma unroll
@@ -620,7 +637,6 @@ void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_
 // tile (P at the tile's first row, M at its first column's row), so every offset stays
 // far below 2^31 whatever the problem size. PRE: the epilogue's U entries are loaded
 // before the K-loop (their latency hidden, 16 more VGPRs).
-typedef __attribute__((address_space(3))) void lds_void;
 template <int NS, bool PRE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4 : 3))) void k_gemm_f32b(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
@@ -668,8 +684,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
   }
 #define ADMMQ_ISSUE(s, kt)                                                                            \
   _Pragma("unroll") for (int j = 0; j < GPW; ++j)                                                    \
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(stp[s] + (wave * GPW + j) * 256), 16, voff[j], \
-                                             (kt) * (BK * 4), 0, 0)
+    blds16(rs, stp[s] + (wave * GPW + j) * 256, voff[j], (kt) * (BK * 4))
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) ADMMQ_ISSUE(s, min(s, nk - 1));
   bool skip = p.flags[0] != 0;

@@ -886,7 +886,7 @@ static int valid_bits(int b) { return b >= 1 && b <= 16; }
 
 static const int g_gemm_stage_env = [] {
   const char* e = std::getenv("ADMMQ_GEMM_F32_STAGE");
-  if (e && *e >= '0' && *e <= '3' && e[1] == 0) g_gemm_f32_stage = *e - '0';
+  if (e && *e >= '0' && *e <= '4' && e[1] == 0) g_gemm_f32_stage = *e - '0';
   const char* u = std::getenv("ADMMQ_EVEN_UNITS");   // diagnostics: 0 = kHistElems x nv stage-1 units
   if (u && u[0] == '0' && u[1] == 0) g_even_units = 0;
   const char* fc = std::getenv("ADMMQ_FIN_CAPACITY");   // diagnostics: admmq_debug_set_fin_capacity
@@ -968,14 +968,15 @@ int32_t admmq_debug_set_gemm_ks(int32_t ks) {
 // 0 = k_gemm's global_load_lds with per-lane 64-bit addresses, 1 = k_gemm_f32b (buffer
 // loads with a scalar K offset, U prefetched), 2 = k_gemm_f32b with a 2-deep
 // ring, 3 = k_gemm_f32b without the U prefetch (the default: C3 mode 0 0.655 -> 0.597 us per
-// 64x64 K-step per CU against 0). ADMMQ_GEMM_F32_STAGE sets it at load time.
+// 64x64 K-step per CU against 0), 4 = 3 with the waves' MFMA bursts at raised issue
+// priority (s_setprio). ADMMQ_GEMM_F32_STAGE sets it at load time.
 int32_t admmq_debug_set_even_units(int32_t on) {
   g_even_units = on != 0;
   return ADMMQ_OK;
 }
 
 int32_t admmq_debug_set_gemm_stage(int32_t v) {
-  if (v < 0 || v > 3) return fail(ADMMQ_ERR_ARG, "stage must be 0..3");
+  if (v < 0 || v > 4) return fail(ADMMQ_ERR_ARG, "stage must be 0..4");
   g_gemm_f32_stage = v;
   return ADMMQ_OK;
 }

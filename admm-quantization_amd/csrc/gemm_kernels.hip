@@ -637,7 +637,7 @@ void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_
 // tile (P at the tile's first row, M at its first column's row), so every offset stays
 // far below 2^31 whatever the problem size. PRE: the epilogue's U entries are loaded
 // before the K-loop (their latency hidden, 16 more VGPRs).
-template <int NS, bool PRE>
+template <int NS, bool PRE, bool PRIO = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4 : 3))) void k_gemm_f32b(
     const ProbDesc* __restrict__ probs, const GemmTile* __restrict__ tiles, int slot, int iter, float eps, int ncand) {
   constexpr int BM = 64, ROWS = 128, STAGE = ROWS * 32, GPW = 4;
@@ -715,6 +715,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
     ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
     const float* st = stp[s];                                                                 \
     float4 fa[2], fb[2];                                                                      \
+    if (PRIO) __builtin_amdgcn_s_setprio(1);                                                  \
     _Pragma("unroll") for (int qq = 0; qq < 4; ++qq) {                                        \
       if (qq == 0) {                                                                          \
         const int cp = ((4 * h) ^ swz) * 4;                                                   \
@@ -735,6 +736,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);                     \
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                      \
     }                                                                                         \
+    if (PRIO) __builtin_amdgcn_s_setprio(0);                                                  \
   } while (0)
   const int nfull = nk / NS * NS;
   for (int kt0 = 0; kt0 < nfull; kt0 += NS) {
@@ -860,6 +862,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
     else if (g_gemm_f32_stage == 1) ADMMQ_LAUNCH((k_gemm_f32b<3, true>), ntiles_big, 256, t);
     else if (g_gemm_f32_stage == 2) ADMMQ_LAUNCH((k_gemm_f32b<2, false>), ntiles_big, 256, t);
     else if (g_gemm_f32_stage == 3) ADMMQ_LAUNCH((k_gemm_f32b<3, false>), ntiles_big, 256, t);
+    else if (g_gemm_f32_stage == 4) ADMMQ_LAUNCH((k_gemm_f32b<3, false, true>), ntiles_big, 256, t);
     else ADMMQ_LAUNCH((k_gemm<2, 1, 3, false>), ntiles_big, 256, t);
   }
   if (ntiles_small > 0) {

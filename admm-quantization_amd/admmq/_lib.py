@@ -107,6 +107,9 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_f32_persistent": (I32, [I32, I32]),
         "admmq_debug_set_gemm_ks": (I32, [I32]),
         "admmq_debug_set_gemm_stage": (I32, [I32]),
+        "admmq_debug_set_ksplit": (I32, [I32]),
+        "admmq_debug_set_ksplit_form": (I32, [I32]),
+        "admmq_debug_ksplit_pieces": (I32, [I32, I32]),
         "admmq_debug_set_even_units": (I32, [I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
         "admmq_debug_set_thin_loop": (I32, [I32]),
@@ -182,6 +185,28 @@ def problems_array(items: Sequence[AdmmProblem]):
 
 def qtensor_array(items: Sequence[QTensor]):
     return (QTensor * len(items))(*items)
+
+
+# Calls repaired on the Python side (the ctypes route, and admmq.factorize's per-sweep
+# repair): see fault_repairs
+_PY_REPAIRS = [0]
+
+
+def note_repair(n: int = 1):
+    _PY_REPAIRS[0] += n
+
+
+def fault_repairs(reset: bool = False) -> int:
+    """Re-runs made because a fused path reported an internal fault (its bounded wait
+    expired: the launch's blocks were not all resident, e.g. another stream's kernels on
+    the device), since the last reset, process-wide: the torch op's own repairs
+    (``torch.ops.admmq.fault_repairs``) plus the Python routes'. 0 on an undisturbed device."""
+    n = _PY_REPAIRS[0]
+    if reset:
+        _PY_REPAIRS[0] = 0
+    if use_ops():
+        n += int(ops().fault_repairs(bool(reset)))
+    return n
 
 
 class exhaustive_search:

@@ -91,8 +91,10 @@ def admm_iteration_batched(problems: Sequence[Tuple[torch.Tensor, torch.Tensor, 
     """Run ``admm_iteration`` on every (H, U, F, G) of ``problems`` in shared launches.
 
     Returns the list of new H tensors (and the caller's U tensors are updated in
-    place). With ``return_info`` also returns an int32 tensor [n, 4] of
-    {iterations run, converged, spd_error, internal fault}; with ``debug_outputs`` a list
+    place). With ``return_info`` also returns an int32 tensor [n, 5] of
+    {iterations run, converged, spd_error, internal fault, re-runs of this call} (the
+    last column is 1 when an internal fault was repaired; ``_lib.fault_repairs`` counts
+    them process-wide); with ``debug_outputs`` a list
     of (H_T, X) of the last iteration per problem. ``solve``: ``"fp32"`` (the process
     default unless ``_lib.solve_mode`` changed it: fp32 MFMA, the reference's arithmetic)
     or ``"split"`` for this call. Calls ``torch.ops.admmq.admm_iteration_batched``
@@ -162,9 +164,15 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
         if int(info.view(n, 4)[:, 2].max().item()) != 0:
             raise torch.linalg.LinAlgError("linalg.cholesky: The factorization could not be completed because "
                                            "the input is not positive-definite.")
+    def info5(reruns=0):
+        out = torch.zeros((n, 5), dtype=torch.int32, device=dev)
+        out[:, :4] = info.view(n, 4)
+        out[:, 4] = reruns
+        return out
+
     if max_iter <= 1:
         outs = [p[0] for p in problems]
-        return (outs, info.view(n, 4)) if return_info else outs
+        return (outs, info5()) if return_info else outs
     outs = [torch.empty_like(h) for h in Hs]
     for it, o in zip(items, outs):
         it.H_out = o.data_ptr()
@@ -176,6 +184,7 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
                                          _lib.ptr(ws), nb, _lib.ptr(info), stream), "admm_run")
 
     run()
+    reruns = 0
     if check_fault and int(info.view(n, 4)[:, 3].max().item()) != 0:   # internal fault: repeat without the fused finalize
         for u, b in zip(Us, ubak):
             u.copy_(b)
@@ -184,6 +193,8 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
         run()
         if int(info.view(n, 4)[:, 3].max().item()) != 0:
             raise RuntimeError("admmq: internal fault in the separate-finalize re-run")
+        reruns = 1
+        _lib.note_repair()
     for u_user, u in zip(Us_user, Us):
         if u is not u_user:
             u_user.copy_(u)
@@ -191,7 +202,7 @@ def _admm_iteration_batched_cabi(problems, max_iter, eps, bits, code, num_attemp
     if debug_outputs:
         ret.append(dbg)
     if return_info:
-        ret.append(info.view(n, 4))
+        ret.append(info5(reruns))
     return ret[0] if len(ret) == 1 else tuple(ret)
 
 

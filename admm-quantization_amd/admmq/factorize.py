@@ -28,7 +28,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
-from . import synthetic
+from . import _lib, synthetic
 from .admm import admm_iteration_batched, init_factors
 from .als import gram_mttkrp, gram_mttkrp_batched, rel_error_batched  # noqa: F401
 from .quantization import quantize_batched
@@ -82,29 +82,50 @@ def als_sweep(runs: Sequence[LayerRun], max_iter_admm: int, eps: float, bits: in
     factor-iterations the inner ADMM loops ran in this sweep, per active layer
     (``{id(run): count}``).
 
-    SPD failures are read once per sweep (one host sync): a ``LinAlgError`` is raised
-    after every mode of the sweep has run, so - unlike the reference, which raises at
-    the Cholesky call before changing anything (``source/admm.py:54``) - the runs'
-    factors, duals and quantized factors are undefined after the error."""
+    SPD failures and internal faults are read once per sweep (one host sync):
+    * a ``LinAlgError`` is raised after every mode of the sweep has run, so - unlike the
+      reference, which raises at the Cholesky call before changing anything
+      (``source/admm.py:54``) - the runs' factors, duals and quantized factors are
+      undefined after the error;
+    * an internal fault of a fused path (its bounded wait expired: another stream's work
+      broke its residency assumption, include/admmq.h) restores the sweep's starting
+      factors, duals and quantized factors and re-runs the whole sweep without the fused
+      paths (later modes read the earlier modes' results, so a faulted call cannot be
+      repeated alone); the repair is counted in ``_lib.fault_repairs``."""
     act = [r for r in runs if r.active]
     nmodes = max((len(r.factors) for r in act), default=0)
-    infos = []
-    for mode in range(nmodes):
-        sel = [r for r in act if mode < len(r.factors)]
-        GF = gram_mttkrp_batched([(r.W, r.factors) for r in sel], mode)
-        probs = [(r.factors[mode], r.duals[mode], F, G) for r, (G, F) in zip(sel, GF)]
-        # no per-call sync for the SPD test: the flags are read once per sweep (below)
-        Hs, info = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
-                                          check_spd=False, return_info=True, solve=solve)
-        infos.append(info[:, [0, 2]])   # {iterations run, spd_error}
-        for r, H in zip(sel, Hs):
-            r.factors[mode] = H
-        qs = quantize_batched(Hs, bits, qscheme, num_attempts=num_attempts)
-        for r, q in zip(sel, qs):
-            r.quantized[mode] = q
+    # the sweep's starting point (factors and quantized factors are rebound, duals updated in place)
+    start = [(list(r.factors), [u.clone() for u in r.duals], list(r.quantized)) for r in act]
+
+    def modes(check_fault):
+        infos = []
+        for mode in range(nmodes):
+            sel = [r for r in act if mode < len(r.factors)]
+            GF = gram_mttkrp_batched([(r.W, r.factors) for r in sel], mode)
+            probs = [(r.factors[mode], r.duals[mode], F, G) for r, (G, F) in zip(sel, GF)]
+            # no per-call sync for the SPD and fault tests: the flags are read once per sweep (below)
+            Hs, info = admm_iteration_batched(probs, max_iter_admm, eps, bits, qscheme, num_attempts=num_attempts,
+                                              check_spd=False, return_info=True, solve=solve, check_fault=check_fault)
+            infos.append(info[:, [0, 2, 3]])   # {iterations run, spd_error, internal fault}
+            for r, H in zip(sel, Hs):
+                r.factors[mode] = H
+            qs = quantize_batched(Hs, bits, qscheme, num_attempts=num_attempts)
+            for r, q in zip(sel, qs):
+                r.quantized[mode] = q
+        return torch.cat(infos).cpu() if infos else None   # the sweep's one host sync for the flags
+
+    both = modes(False)
+    if both is not None and int(both[:, 2].max()) != 0:   # internal fault: the sweep again, without the fused paths
+        for r, (fs, us, qs) in zip(act, start):
+            r.factors[:] = fs
+            for u, u0 in zip(r.duals, us):
+                u.copy_(u0)
+            r.quantized[:] = qs
+        with _lib.fused_finalize(False):
+            both = modes(True)
+        _lib.note_repair()
     iters = {id(r): 0 for r in act}
-    if infos:
-        both = torch.cat(infos).cpu()   # the sweep's one host sync for the flags
+    if both is not None:
         check_spd_flags([both[:, 1]], act, nmodes)
         k = 0
         for mode in range(nmodes):

@@ -101,7 +101,9 @@ class KrylovProjector:
     def __call__(self, X: torch.Tensor) -> torch.Tensor:
         m, n = X.shape
         r = min(self.rank, m, n)
-        k = min(self.block, m, n)
+        # blocks at least `rank` wide: the first Rayleigh-Ritz check then already has r Ritz
+        # pairs (a narrower K would index past its eigenpairs and wrap to the top ones)
+        k = min(max(self.block, r), m, n)
         Xd = X.double()
         if self.Q is None or self.Q.shape != (m, k):
             g = torch.Generator().manual_seed(self.seed)
@@ -127,7 +129,7 @@ class KrylovProjector:
                 continue
             B = K.T @ Xd                                   # (nb k) x n
             evals, evecs = torch.linalg.eigh(B @ B.T)      # ascending
-            idx = torch.arange(evals.shape[0] - 1, evals.shape[0] - 1 - max(k, r), -1, device=X.device)
+            idx = torch.arange(evals.shape[0] - 1, evals.shape[0] - 1 - k, -1, device=X.device)   # k <= K's columns
             S = torch.sqrt(torch.clamp(evals[idx], min=0.0))
             Ub = evecs[:, idx]
             U = K @ Ub[:, :r]

@@ -87,7 +87,9 @@ struct ProbDesc {
   int nq;          // quads of the valid (I x R) region: I * ceil(R/4)
   int split;       // 1: this problem's solve uses the split operand planes
   int fin_rows;    // split: rows per finalize unit (units hold whole rows)
-  int pad_;
+  int ksplit;      // K-split pieces of each 64 x 64 solve tile (1: none); a function of (I, R) only
+  float* kpart;    // K-split: partial images [tiles][ksplit][4096] floats
+  unsigned* kctr;  // K-split: per-tile arrival counters (monotonic, zeroed per run)
 };
 
 // A standalone quantization job (quantize_tensor): x viewed as (rows, cols).
@@ -106,12 +108,24 @@ struct QJob {
 // and strides ride along (filled at upload), so a tile's first loads depend on the
 // tile entry only, not on a further descriptor read. Split form: P / M point at the
 // fp16 planes (row strides in floats are unchanged), eP / eM at the row exponents.
+// K-split pieces (fp32 64 x 64 tiles; the piece count np is fixed by the factor's shape:
+// api.hip ksplit_pieces): piece p covers K-steps [p nk / np, (p + 1) nk / np) of the tile
+// in its own accumulator chain and the tile is ((p0 + p1) + p2) + ... Two execution forms
+// with the same bits: parallel (launches that leave CUs idle: np workgroups per tile, piece
+// pc of np runs K-steps [k0, k0 + nk), `part` holds the tile's np partial images, `ctr` its
+// arrival counter: gemm_kernels.hip ksplit_combine) or serial (one workgroup runs the whole
+// tile and folds its accumulator into the running sum at each of the ser - 1 piece starts).
 struct GemmTile {
   int prob, tm, tn, first, nk, bm;   // bm: tile rows of the persistent fp32 kernel (k_gemm_f32p), else 0
   const float* P; const float* M; const float* U;
   const int* eP; const int* eM;
   int ld, ldm;
+  int k0, np, pc, ser;               // K-split: parallel form: first K-step, pieces, this piece (np = 1: whole tile);
+                                     // serial form: pieces folded in this workgroup (1: none)
+  float* part; unsigned* ctr;        // K-split: the tile's partial images [np][16 KB] and arrival counter
 };
+constexpr int kKsplitMax = 4;        // pieces per tile at most
+constexpr int kKsplitMinSteps = 6;   // K-steps per piece at least
 // Thin-factor solve workgroup (thin_loop.hip): columns [col0, col0 + cw) of problem `job`,
 // the rank-th of the problem's nteam workgroups (in the persistent loop rank 0 resets the
 // team's words)

@@ -109,6 +109,37 @@ static int f32_tile_rows(int I, int ld) {
 }
 static constexpr int kF32Slots = 2;   // k_gemm_f32p workgroups per CU (72 KB of LDS each)
 
+// K-split of the fp32 64 x 64 solve tiles (gemm_kernels.hip ksplit_combine): 1 = by
+// ksplit_pieces, 0 = never (A/B). A factor whose tiles alone leave most of the chip idle
+// (a lone layer4 conv: 144 tiles of 36 K-steps on 256 CUs, the busiest shard of a
+// multi-GPU run) splits every tile's K range into np pieces summed in piece order.
+static std::atomic<int> g_ksplit{1};
+// execution form of the pieces (same bits either way): 1 = parallel only where the 64 x 64
+// launch's whole tiles leave CUs idle, else serial (default); 0 = always serial; 2 = always parallel
+static std::atomic<int> g_ksplit_par{1};
+// Pieces per tile, a function of (I, R) ONLY (never of the batch, the device or the
+// launch), so a factor's bits are the same in every batch: the np in 1..kKsplitMax with
+// pieces of >= kKsplitMinSteps K-steps that minimises the factor's own launch length on
+// a 256-CU chip, ceil(tiles np / 256) ceil(nk / np) K-steps plus kKsplitCost for the
+// partial hand-off, ties to the smaller np. Only factors with fewer tiles than CUs split.
+static constexpr int kKsplitChipCUs = 256;
+static constexpr int kKsplitCost = 4;   // K-steps (~2.5 us): partial stores, arrival, sc1 reads
+static int ksplit_pieces(int I, int R) {
+  if (I <= 32) return 1;   // 32 x 64 tiles
+  const int nk = rup(R, 32) / 32;
+  const long long tiles = (long long)((I + 63) / 64) * ((rup(R, 32) + 63) / 64);
+  if (tiles >= kKsplitChipCUs) return 1;
+  int best = 1;
+  long long best_cost = nk;
+  for (int np = 2; np <= kKsplitMax; ++np) {
+    const int len = (nk + np - 1) / np;
+    if (len < kKsplitMinSteps) break;
+    const long long cost = (tiles * np + kKsplitChipCUs - 1) / kKsplitChipCUs * len + kKsplitCost;
+    if (cost < best_cost) { best = np; best_cost = cost; }
+  }
+  return best;
+}
+
 // CUs of the current device (looked up once per device)
 static int device_cus() {
   constexpr int kMaxDev = 64;
@@ -171,18 +202,29 @@ static void plan_f32_lists(std::vector<GemmTile>& tiles, std::vector<int>& off, 
   off[nslots] = (int)tiles.size();
 }
 
-// Solve mode recorded by each prepare for its workspace (the run must use the operand
-// planes its prepare wrote: the per-problem buffer carve depends on the mode).
+// What each prepare recorded for its workspace: the solve mode (the run must use the operand
+// planes its prepare wrote) and a fingerprint of the carve - the problem shapes, the byte
+// count and every process switch that moves buffers (tile rows, stage-1 unit sizing,
+// K-split) - so a run whose plan would carve the workspace differently is refused instead of
+// reading another layout. Keyed by address: a workspace freed and reallocated at the same
+// address for the same problems still needs its own prepare (include/admmq.h).
+struct WsRecord { int mode; unsigned long long fp; };
 static std::mutex g_ws_mu;
-static std::unordered_map<const void*, int> g_ws_mode;
-static void record_ws_mode(const void* ws, int mode) {
+static std::unordered_map<const void*, WsRecord> g_ws_rec;
+static void record_ws(const void* ws, int mode, unsigned long long fp) {
   std::lock_guard<std::mutex> g(g_ws_mu);
-  g_ws_mode[ws] = mode;
+  g_ws_rec[ws] = {mode, fp};
+}
+static bool recorded_ws(const void* ws, WsRecord& out) {
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  auto it = g_ws_rec.find(ws);
+  if (it == g_ws_rec.end()) return false;
+  out = it->second;
+  return true;
 }
 static int recorded_ws_mode(const void* ws) {
-  std::lock_guard<std::mutex> g(g_ws_mu);
-  auto it = g_ws_mode.find(ws);
-  return it == g_ws_mode.end() ? -1 : it->second;
+  WsRecord r;
+  return recorded_ws(ws, r) ? r.mode : -1;
 }
 
 // The two-stage search needs the per-block threshold table in LDS; otherwise exhaustive.
@@ -313,6 +355,9 @@ struct AdmmPlan {
   int nfin_big = 0, nhist_big = 0;   // finalize / stage-1 units of the other jobs (listed first)
   bool rows_aligned = true;          // every big job's stage-1 units are whole rows (fused finalize possible)
   unsigned* d_ready = nullptr;       // [nprob][2] fused-finalize ready words (zeroed per run)
+  unsigned* d_kctr = nullptr;        // K-split arrival counters (zeroed per run)
+  size_t nkctr = 0;
+  bool ksplit_par = false;           // this launch runs the K-split pieces in parallel (else serially)
   int small_groups = 0;              // float4 groups per thread of the fused kernel (0: too large)
   // persistent thin-factor loop (k_thin_loop, one team of workgroups per problem): possible
   // when every problem is thin, ld <= 1152 and the workgroups fit the CUs (64-column
@@ -325,7 +370,9 @@ struct AdmmPlan {
 
 static GemmTile mk_tile(int prob, int tm, int tn, int first, int nk) {
   GemmTile t;
+  std::memset(&t, 0, sizeof(t));
   t.prob = prob; t.tm = tm; t.tn = tn; t.first = first; t.nk = nk; t.bm = 0;
+  t.k0 = 0; t.np = 1; t.pc = 0; t.ser = 1;
   t.P = nullptr; t.M = nullptr; t.U = nullptr; t.eP = nullptr; t.eM = nullptr; t.ld = 0; t.ldm = 0;   // set at upload
   return t;
 }
@@ -451,6 +498,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       if (probs[i].I > 32) t64 += (long long)((probs[i].I + 63) / 64) * ((rup(std::max(probs[i].R, 1), 32) + 63) / 64);
     pl.wide = t64 >= kWideMinTiles;
   }
+  auto wide_prob = [&](const ProbDesc& d) { return pl.wide && d.I > 64 && d.ksplit == 1; };
   for (int i = 0; i < nprob; ++i)   // the split finalize needs whole rows in one unit
     if (probs[i].I > kThinRows && rup(std::max(probs[i].R, 1), 32) > 8192) pl.split = false;
   for (int i = 0; i < nprob; ++i) {
@@ -463,8 +511,12 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     d.HT_dbg = a.HT_out; d.X_dbg = a.X_out;
     d.I = a.I; d.R = a.R;
     d.ld = rup(a.R, 32);
-    const bool f32p_prob = !pl.split && g_f32_kernel.load() != 0 && !(pl.wide && a.I > 64) && a.I > kThinRows;
-    d.Ip = a.I <= 32 ? 32 : rup(a.I, (pl.wide && a.I > 64) ? kWideRows : (f32p_prob ? std::max(64, f32_tile_rows(a.I, rup(a.R, 32))) : 64));
+    // K-split pieces (fp32 64 x 64 tiles only; by shape alone): such a factor never takes
+    // the wide tiles, whatever its launch, so its bits stay those of its own shape
+    d.ksplit = (!pl.split && g_ksplit.load() != 0 && g_f32_kernel.load() == 0 && g_gemm_ks_f32 == 1 &&
+                a.I > kThinRows) ? ksplit_pieces(a.I, a.R) : 1;
+    const bool f32p_prob = !pl.split && g_f32_kernel.load() != 0 && !wide_prob(d) && a.I > kThinRows;
+    d.Ip = a.I <= 32 ? 32 : rup(a.I, wide_prob(d) ? kWideRows : (f32p_prob ? std::max(64, f32_tile_rows(a.I, rup(a.R, 32))) : 64));
     d.ldm = rup(a.R, 64);
     d.nbk = d.ldm / 32;
     d.nq = a.I * ((a.R + 3) / 4);
@@ -484,6 +536,10 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
       d.eP = cv.take<int>(d.Ip);
       d.M2 = cv.take<_Float16>(2 * (size_t)d.ldm * d.ldm);
       d.eM = cv.take<int>(d.ldm);
+    }
+    if (d.ksplit > 1) {   // the partial images of every 64 x 64 tile (the counters are carved below)
+      const long long nt = (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
+      d.kpart = cv.take<float>((size_t)nt * d.ksplit * 4096);
     }
     d.res = cv.take<double>(2 * kResRep * 4);
     d.flags = cv.take<int>(4);
@@ -519,7 +575,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     std::vector<long long> qload(kXcd, 0);
     for (int i : order) {
       const ProbDesc& d = pl.desc[i];
-      if (!(pl.wide && d.I > 64)) continue;
+      if (!wide_prob(d)) continue;
       const int TM = d.Ip / kWideRows, TN = (d.ld + 127) / 128;
       for (int tm = 0; tm < TM; ++tm) {
         const int x = (int)(std::min_element(qload.begin(), qload.end()) - qload.begin());
@@ -552,7 +608,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     std::vector<GemmTile> ft;
     for (int i : order) {
       const ProbDesc& d = pl.desc[i];
-      if (d.I <= kThinRows || (pl.wide && d.I > 64)) continue;
+      if (d.I <= kThinRows || wide_prob(d)) continue;
       const int bm = f32_tile_rows(d.I, d.ld);
       const int TM = (d.I + bm - 1) / bm, TN = (d.ld + 63) / 64;
       for (int tm = 0; tm < TM; ++tm)
@@ -572,7 +628,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   if (pl.f32t) {
     for (int i : order) {
       const ProbDesc& d = pl.desc[i];
-      if (d.I <= kThinRows || (pl.wide && d.I > 64)) continue;
+      if (d.I <= kThinRows || wide_prob(d)) continue;
       const int bm = f32_tile_rows(d.I, d.ld);
       const int TM = (d.I + bm - 1) / bm, TN = (d.ld + 63) / 64;
       for (int tm = 0; tm < TM; ++tm)
@@ -585,17 +641,52 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     order_tiles_for_cus(pl.tiles, 256, 3);
     pl.ntiles_f32t = (int)pl.tiles.size();
   }
+  // K-split arrival counters: one per split tile, contiguous (zeroed at the start of every run)
+  pl.nkctr = 0;
+  for (int i = 0; i < nprob; ++i)
+    if (pl.desc[i].ksplit > 1) pl.nkctr += (size_t)(pl.desc[i].Ip / 64) * ((pl.desc[i].ld + 63) / 64);
+  pl.d_kctr = cv.take<unsigned>(std::max<size_t>(pl.nkctr, 1));
+  // The K-split pieces of a factor (fixed by its shape) run in parallel, np workgroups per
+  // tile, only in a launch whose whole tiles leave CUs idle (a lone large factor, as in a
+  // multi-GPU shard); otherwise one workgroup folds them serially (same bits, no hand-off).
+  long long whole64 = 0;
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
+    whole64 += (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
+  }
+  pl.ksplit_par = g_ksplit_par.load() == 2 || (g_ksplit_par.load() == 1 && whole64 <= kKsplitChipCUs);
+  size_t nctr = 0;
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     if (pl.f32p || pl.f32t) break;
-    if (d.I <= kThinRows || d.Ip == 32 || (pl.wide && d.I > 64)) continue;   // thin / 32-row / wide: elsewhere
+    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;   // thin / 32-row / wide: elsewhere
     const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
+    const int nk = d.ld / 32, np = pl.ksplit_par ? d.ksplit : 1;
     for (int g0 = 0; g0 < TN; g0 += 8)
       for (int tm = 0; tm < TM; ++tm)
         for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
-          pl.tiles.push_back(mk_tile(i, tm, tn, (tm == 0 && tn == 0) ? 1 : 0, d.ld / 32));
+          for (int pc = 0; pc < np; ++pc) {   // parallel K-split pieces: [pc nk / np, (pc + 1) nk / np)
+            const int k0 = pc * nk / np, k1 = (pc + 1) * nk / np;
+            GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0 && pc == 0) ? 1 : 0, k1 - k0);
+            if (np > 1) {
+              t.k0 = k0; t.np = np; t.pc = pc;
+              t.part = d.kpart + (size_t)(tm * TN + tn) * np * 4096;
+              t.ctr = pl.d_kctr + (size_t)(nctr + tm * TN + tn);
+            } else {
+              t.ser = d.ksplit;   // serial form (1: no K-split)
+            }
+            pl.tiles.push_back(t);
+          }
+    if (d.ksplit > 1) nctr += TM * TN;
   }
-  if (!pl.f32p && !pl.f32t) order_tiles_for_cus(pl.tiles, 256, 3);
+  if (!pl.f32p && !pl.f32t) {
+    // a launch of more tiles than resident slots (K-split pieces, C4) is dispatched in
+    // order as slots free up: longest first (a no-op without pieces: problems are in ld order)
+    if (pl.tiles.size() > 256 * 3)
+      std::stable_sort(pl.tiles.begin(), pl.tiles.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
+    order_tiles_for_cus(pl.tiles, 256, 3);
+  }
   std::vector<GemmTile> small;
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
     const ProbDesc& d = pl.desc[i];
@@ -739,6 +830,25 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_groups = cv.take<unsigned short>(3 * kMaxMerged);
   pl.bytes = align_up(cv.off, 256);
   return ADMMQ_OK;
+}
+
+// Fingerprint of a plan's carve (FNV-1a over the byte count, the shapes and the offsets of
+// each problem's buffers from the workspace base): equal iff prepare and run lay it out alike
+static unsigned long long plan_fingerprint(const AdmmPlan& pl, const void* ws) {
+  unsigned long long h = 1469598103934665603ull;
+  auto mix = [&](long long v) {
+    for (int b = 0; b < 8; ++b) { h ^= (unsigned long long)((v >> (8 * b)) & 0xFF); h *= 1099511628211ull; }
+  };
+  const char* base = static_cast<const char*>(ws);
+  auto off = [&](const void* p) { return p ? (long long)(static_cast<const char*>(p) - base) : -1LL; };
+  mix((long long)pl.bytes);
+  mix((long long)pl.desc.size());
+  for (const ProbDesc& d : pl.desc) {
+    mix(d.I); mix(d.R); mix(d.Ip); mix(d.ld); mix(d.ldm); mix(d.split); mix(d.ksplit);
+    mix(off(d.Fp)); mix(off(d.M)); mix(off(d.P2)); mix(off(d.kpart)); mix(off(d.mv.h1)); mix(off(d.flags));
+  }
+  mix(off(pl.d_desc)); mix(off(pl.d_tiles)); mix(off(pl.d_kctr)); mix(off(pl.d_rank0));
+  return h;
 }
 
 static int upload_admm(AdmmPlan& pl, hipStream_t s) {
@@ -981,6 +1091,26 @@ int32_t admmq_debug_set_gemm_stage(int32_t v) {
   return ADMMQ_OK;
 }
 
+// diagnostics (not in include/admmq.h): K-split of the fp32 64 x 64 solve tiles by the
+// factor's shape (1, default) or never (0; changes the bits of the factors that split)
+int32_t admmq_debug_set_ksplit(int32_t on) {
+  if (on < 0 || on > 1) return fail(ADMMQ_ERR_ARG, "ksplit must be 0 or 1");
+  g_ksplit = on;
+  return ADMMQ_OK;
+}
+// diagnostics: execution form of the K-split pieces (same bits): 1 = parallel where the launch
+// leaves CUs idle (default), 0 = always serial (one workgroup per tile), 2 = always parallel
+int32_t admmq_debug_set_ksplit_form(int32_t form) {
+  if (form < 0 || form > 2) return fail(ADMMQ_ERR_ARG, "ksplit form must be 0..2");
+  g_ksplit_par = form;
+  return ADMMQ_OK;
+}
+// diagnostics: the K-split pieces the planner gives an (I, R) factor (0 on bad arguments)
+int32_t admmq_debug_ksplit_pieces(int32_t I, int32_t R) {
+  if (I <= 0 || R <= 0) return 0;
+  return ksplit_pieces(I, R);
+}
+
 int32_t admmq_debug_set_f32_persistent(int32_t kernel, int32_t rule) {
   if (rule < 0 || rule > 3) return fail(ADMMQ_ERR_ARG, "rule must be 0..3");
   if (kernel < 0 || kernel > 2) return fail(ADMMQ_ERR_ARG, "kernel must be 0..2");
@@ -1088,7 +1218,7 @@ int32_t admmq_admm_prepare_ex(const admmq_problem* probs, int32_t nprob, int32_t
   }
   prof_mark(s);
   if ((rc = check_hip("admm_prepare"))) return rc;
-  record_ws_mode(workspace, opt->solve_mode);
+  record_ws(workspace, opt->solve_mode, plan_fingerprint(pl, workspace));
   return ADMMQ_OK;
 }
 
@@ -1105,16 +1235,22 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   if (rc) return rc;
   if (!valid_scheme(qscheme)) return fail(ADMMQ_ERR_SCHEME, "unknown qscheme");
   if (!valid_bits(bits)) return fail(ADMMQ_ERR_ARG, "bits out of range");
-  const int rec = recorded_ws_mode(workspace);
-  if (rec < 0) return fail(ADMMQ_ERR_ARG, "admm_run: the workspace has not been prepared (admmq_admm_prepare)");
+  WsRecord wr;
+  if (!recorded_ws(workspace, wr))
+    return fail(ADMMQ_ERR_ARG, "admm_run: the workspace has not been prepared (admmq_admm_prepare)");
+  const int rec = wr.mode;
   if (rec != opt->solve_mode) return fail(ADMMQ_ERR_ARG, "admm_run: solve_mode differs from the one its prepare used");
   AdmmPlan pl;
   rc = plan_admm(probs, nprob, num_attempts, workspace, pl, rec);
   if (rc) return rc;
   if (!workspace || workspace_bytes < pl.bytes) return fail(ADMMQ_ERR_WORKSPACE, "workspace too small");
+  if (plan_fingerprint(pl, workspace) != wr.fp)
+    return fail(ADMMQ_ERR_ARG, "admm_run: the problems or layout switches differ from the workspace's prepare");
   hipStream_t s = static_cast<hipStream_t>(stream);
   // descriptors carry this call's output pointers (H_out may differ from prepare's)
   if ((rc = upload_admm(pl, s))) return rc;
+  if (pl.nkctr > 0 && hipMemsetAsync(pl.d_kctr, 0, pl.nkctr * sizeof(unsigned), s) != hipSuccess)
+    return check_hip("K-split counter reset");
   const int nsse = (int)pl.sse_chunks.size(), nfin = (int)pl.fin_chunks.size();
   const int nhist = (int)pl.hist_chunks.size();
   const bool exhaustive = !two_stage_ok(num_attempts, bits);
@@ -1131,7 +1267,10 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   // the big jobs' finalize inside the search launch when all its blocks fit at once
   // (with a margin of one resident block per CU: see hist3_fin_capacity)
   const int nh_big = fuse_small ? pl.nhist_big : nhist;
-  const bool fin_ok = opt->fused_finalize && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0;
+  // the fused paths report a broken residency assumption only through info: without it
+  // they never run (include/admmq.h)
+  const bool fused_allowed = opt->fused_finalize != 0 && info != nullptr;
+  const bool fin_ok = fused_allowed && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0;
   const int cap_over = g_fin_cap_override.load();
   const int fin_cap = fin_ok ? (cap_over > 0 ? std::min(cap_over, hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
                                              : hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
@@ -1174,7 +1313,7 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   // every problem thin: all iterations in one persistent launch (k_thin_loop) when the
   // fused paths are allowed (the op's fault retry turns them off) and it fits the device
   bool loop_done = false;
-  if (pl.tl_ok && g_thin_loop.load() != 0 && opt->fused_finalize && qscheme == kMse && !exhaustive && max_iter > 1 &&
+  if (pl.tl_ok && g_thin_loop.load() != 0 && fused_allowed && qscheme == kMse && !exhaustive && max_iter > 1 &&
       num_attempts >= 2 && num_attempts <= kTLMaxCand && bits >= 2 && bits <= 5) {
     if ((rc = h2d(pl.d_tl_units, pl.tl_units.data(), pl.tl_units.size() * sizeof(ThinLoopUnit), s))) return rc;
     if (hipMemsetAsync(pl.d_tl_sync, 0, (size_t)nprob * sizeof(ThinSync), s) != hipSuccess)

@@ -109,6 +109,57 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 __device__ __forceinline__ f16x8 as_h8(float4 v) { return __builtin_bit_cast(f16x8, v); }
 
+// K-split combine of a 64 x 64 fp32 tile (4 waves, 256 threads, one f32x16 accumulator
+// per thread in the 32x32x2 C/D layout; api.hip ksplit_pieces). Piece pc of np has summed
+// K-steps [k0, k0 + nk) of the tile. Every piece publishes its partial: 4 x 16-B sc1
+// (write-through) stores per thread into slot pc of the tile's partial images, laid out
+// by thread, so each thread later reads back exactly the elements it owns; each storing
+// wave drains them (vmcnt(0)) before the workgroup barrier behind which one lane adds to
+// the tile's arrival counter (agent scope). The workgroup whose add completes the tile
+// (the counter advances by np per iteration: (old + 1) % np == 0) reads the other slots
+// with sc1 loads after a barrier its lane joined (MI355X_MICROARCH.md, inter-workgroup
+// visibility, first row) and forms ((p0 + p1) + p2) + ... in piece order - the same float32
+// additions whichever piece arrives last, so the tile's bits are fixed by (I, R) alone.
+// Returns false for the other pieces (they end without an epilogue).
+typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bool ksplit_combine(const GemmTile& tl, f32x16& acc, int* lds_last) {
+  const int tid = threadIdx.x;
+  const int np = tl.np, pc = tl.pc;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tl.part, 0, np * 16384, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const u32x4g w = {__float_as_uint(acc[4 * q]), __float_as_uint(acc[4 * q + 1]), __float_as_uint(acc[4 * q + 2]),
+                      __float_as_uint(acc[4 * q + 3])};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, ((pc * 4 + q) * 256 + tid) * 16, 0, 16);   // sc1
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(tl.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_last = ((old + 1u) % (unsigned)np) == 0u ? 1 : 0;
+  }
+  __syncthreads();
+  if (!*lds_last) return false;
+  u32x4g v[kKsplitMax][4];
+#pragma unroll
+  for (int s = 0; s < kKsplitMax; ++s)
+    if (s < np && s != pc)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[s][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((s * 4 + q) * 256 + tid) * 16, 0, 16);
+  f32x16 sum;
+#pragma unroll
+  for (int s = 0; s < kKsplitMax; ++s) {
+    if (s >= np) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float x = s == pc ? acc[r] : __uint_as_float(v[s][r >> 2][r & 3]);
+      sum[r] = s == 0 ? x : sum[r] + x;
+    }
+  }
+  acc = sum;
+  return true;
+}
+
 // Diagnostics (make TRACE=1 only): per workgroup of the last k_gemm launch {start, end,
 // (block << 48) | (K-steps << 40) | (XCC_ID << 32) | HW_ID} (admmq_debug_gemm_trace, tools/gemm_timeline.py)
 constexpr int kGemmTraceMax = 8192;
@@ -200,10 +251,11 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
   // K-step's byte offset in an SGPR - no VALU address arithmetic in the K-loop (the fp32
   // MFMA shares the VALU's pipe; k_gemm_f32b). A piece is 8 image rows,
   // all P rows or all M rows (BM is a multiple of 8), so its descriptor is wave-uniform.
+  // (a K-split piece, fp32 64 x 64 tiles only, starts at K-step k0: 128 B per K-step in both forms)
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.P + (size_t)row0 * ld), 0, 0x7FFFFFFF, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.P + (size_t)row0 * ld + tl.k0 * BK), 0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.M + (size_t)col0 * ldm), 0, 0x7FFFFFFF, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(tl.M + (size_t)col0 * ldm + tl.k0 * BK), 0, 0x7FFFFFFF, 0x00020000);
   unsigned voff[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
@@ -239,11 +291,15 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
     if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
   }
 
-  f32x16 acc[CW];
+  f32x16 acc[CW], psum;
 #pragma unroll
   for (int c = 0; c < CW; ++c)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[c][r] = psum[r] = 0.f;
+  // serial K-split (fp32 64 x 64 tiles only: k_gemm_f32b's fold, the same order)
+  constexpr bool FOLD = !SPLIT && WM == 2 && KS == 1 && CW == 1;
+  const int ser = FOLD ? tl.ser : 1;
+  int pf = 1, kb = ser > 1 ? nk / ser : nk;
 
   // Per K-step kt on stage s = kt % NS: wait for it (counted vmcnt: the NS-2 later
   // stages stay in flight), publish it (barrier), refill the stage consumed one step
@@ -258,6 +314,14 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
     raw_barrier();                                                                            \
     if (ADMMQ_GEMM_DIAG != 2 || SPLIT) ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1)); \
+    if (FOLD && (kt) == kb && (kt) > 0) {                                                     \
+      _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                        \
+        psum[r] = pf == 1 ? acc[0][r] : psum[r] + acc[0][r];                                  \
+        acc[0][r] = 0.f;                                                                      \
+      }                                                                                       \
+      ++pf;                                                                                   \
+      kb = pf * nk / ser;                                                                     \
+    }                                                                                         \
     const float* st = stp[s];                                                                 \
     if constexpr (SPLIT) {                                                                    \
       _Pragma("unroll") for (int q = 0; q < KCW; ++q) {                                       \
@@ -330,6 +394,15 @@ __global__ __launch_bounds__(128 * WM * KS) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[0][r] += s2[r * 64 + lane];
       }
+    }
+  }
+  if constexpr (FOLD) {   // K-split: the serial form's last piece, or a parallel piece (k_gemm_f32b's combine)
+    if (ser > 1)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] = psum[r] + acc[0][r];
+    if (tl.np > 1) {
+      __shared__ int klast;
+      if (!ksplit_combine(tl, acc[0], &klast)) return;
     }
   }
 
@@ -671,10 +744,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
     }
   };
   if constexpr (PRE) load_u();
-  // waves 0, 1 stage the 64 P rows (image rows 0..63), waves 2, 3 the 64 M rows
+  // waves 0, 1 stage the 64 P rows (image rows 0..63), waves 2, 3 the 64 M rows; a K-split
+  // piece starts at K-step k0 (the descriptors' bases move along the rows)
   const bool isA = wave < 2;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      isA ? (void*)(tl.P + (size_t)row0 * ld) : (void*)(tl.M + (size_t)col0 * ldm), 0, 0x7FFFFFFF, 0x00020000);
+      isA ? (void*)(tl.P + (size_t)row0 * ld + tl.k0 * BK) : (void*)(tl.M + (size_t)col0 * ldm + tl.k0 * BK), 0,
+      0x7FFFFFFF, 0x00020000);
   unsigned voff[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
@@ -704,15 +779,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
     for (int c = tid; c < kHistRep * (ncand + 1); c += 256) { h1[c] = 0ull; h2[c] = 0ull; }
     if (tid == 0) { p.mv.s2[slot] = 0.0; p.mv.ticket[slot] = 0u; }
   }
-  f32x16 acc;
+  f32x16 acc, psum;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = psum[r] = 0.f;
+  // serial K-split (tl.ser pieces): at the first K-step of piece pf, fold the finished
+  // piece into the running sum ((p0 + p1) + ...: ksplit_combine's order) and restart
+  const int ser = tl.ser;
+  int pf = 1, kb = ser > 1 ? nk / ser : nk;
 #define ADMMQ_STEP(s, kt)                                                                     \
   do {                                                                                        \
     wait_vmcnt<GPW * (NS - 2)>();                                                             \
     __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): reads of the refilled stage done */    \
     raw_barrier();                                                                            \
     ADMMQ_ISSUE(((s) + NS - 1) % NS, min((kt) + NS - 1, nk - 1));                             \
+    if ((kt) == kb && (kt) > 0) {                                                             \
+      _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                        \
+        psum[r] = pf == 1 ? acc[r] : psum[r] + acc[r];                                        \
+        acc[r] = 0.f;                                                                         \
+      }                                                                                       \
+      ++pf;                                                                                   \
+      kb = pf * nk / ser;                                                                     \
+    }                                                                                         \
     const float* st = stp[s];                                                                 \
     float4 fa[2], fb[2];                                                                      \
     if (PRIO) __builtin_amdgcn_s_setprio(1);                                                  \
@@ -749,6 +836,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
 #undef ADMMQ_STEP
 #undef ADMMQ_ISSUE
   wait_vmcnt<0>();   // the refills past the end land before the workgroup ends
+  if (ser > 1) {     // serial K-split: the last piece
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = psum[r] + acc[r];
+  }
+  if (tl.np > 1) {   // K-split piece: only the piece that completes the tile goes on
+    __shared__ int klast;
+    if (!ksplit_combine(tl, acc, &klast)) return;
+  }
   if constexpr (!PRE) load_u();
   unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
   typedef __attribute__((address_space(1))) float gf32;

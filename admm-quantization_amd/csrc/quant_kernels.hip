@@ -67,14 +67,17 @@ __global__ __launch_bounds__(256) void k_qfinal(const QJob* __restrict__ jobs, c
 // Per-channel schemes (channel_symmetric / channel_affine with an explicit dim,
 // source/quantization.py:29-33, 91-106). The tensor is viewed as (A, C, B) around the
 // channel dimension dim (C = shape[dim]); channel r = row r of unfold(x, dim)
-// (source/utils.py:60-74). One block per channel: min / max as order-preserving
-// encodings, plus a NaN flag (torch's max / min propagate NaN).
+// (source/utils.py:60-74). gridDim.y blocks per channel (large channels split over
+// several), merged by atomics into stats zeroed beforehand: {~min, max} as order-preserving
+// encodings (min stored complemented so every word starts at 0), plus a NaN flag (torch's
+// max / min propagate NaN).
 __global__ __launch_bounds__(256) void k_channel_stats(const float* __restrict__ x, long long A, int C, long long B,
                                                        unsigned* __restrict__ stats) {
   const int r = blockIdx.x;
   const long long n = A * B;
   unsigned mn = 0xFFFFFFFFu, mxo = 0u, nan = 0u;
-  for (long long t = threadIdx.x; t < n; t += blockDim.x) {
+  const long long step = (long long)blockDim.x * gridDim.y;
+  for (long long t = (long long)blockIdx.y * blockDim.x + threadIdx.x; t < n; t += step) {
     const long long a = t / B, b = t - a * B;
     const float v = x[(a * C + r) * B + b];
     if (v != v) {
@@ -94,33 +97,45 @@ __global__ __launch_bounds__(256) void k_channel_stats(const float* __restrict__
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       mn = min(mn, red[0][k]); mxo = max(mxo, red[1][k]); nan = max(nan, red[2][k]);
     }
-    stats[3 * r + 0] = mn;
-    stats[3 * r + 1] = mxo;
-    stats[3 * r + 2] = nan;
+    atomicMax(&stats[3 * r + 0], ~mn);
+    atomicMax(&stats[3 * r + 1], mxo);
+    atomicMax(&stats[3 * r + 2], nan);
   }
 }
 
 // y (outer x Lo) = the scheme applied to x (outer x L) with the statistics of channel
 // (C == 1 ? 0 : j) for output column j: torch broadcasts the (C,) statistics against the
 // tensor's last dimension (the host checked L == C or one of them is 1; Lo = max(L, C)).
+// Grid-stride over the outputs (the grid is capped; outputs may exceed 2^32).
 __global__ __launch_bounds__(256) void k_channel_quant(const float* __restrict__ x, float* __restrict__ y,
                                                        long long nout, int L, int Lo, int C,
                                                        const unsigned* __restrict__ stats, int bits, int scheme) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nout) return;
-  const long long o = i / Lo;
-  const int j = (int)(i - o * Lo);
-  const int ci = C == 1 ? 0 : j;
-  const float tmin = dec_ord(stats[3 * ci + 0]), tmax = dec_ord(stats[3 * ci + 1]);
-  const QParams qp = qparams_stats(scheme, bits, tmin, tmax, (int)stats[3 * ci + 2], 0, 0.f, 0.f);
-  y[i] = apply_quant(x[o * L + (L == 1 ? 0 : j)], qp);
+  const long long step = (long long)blockDim.x * gridDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += step) {
+    const long long o = i / Lo;
+    const int j = (int)(i - o * Lo);
+    const int ci = C == 1 ? 0 : j;
+    const float tmin = dec_ord(~stats[3 * ci + 0]), tmax = dec_ord(stats[3 * ci + 1]);
+    const QParams qp = qparams_stats(scheme, bits, tmin, tmax, (int)stats[3 * ci + 2], 0, 0.f, 0.f);
+    y[i] = apply_quant(x[o * L + (L == 1 ? 0 : j)], qp);
+  }
 }
 
 void launch_channel_quant(const float* x, float* y, long long A, int C, long long B, long long outer, int L, int Lo,
                           unsigned* stats, int bits, int scheme, hipStream_t s) {
-  hipLaunchKernelGGL(k_channel_stats, dim3(C), dim3(256), 0, s, x, A, C, B, stats);
+  // blocks per channel: about 16 k elements each, at most 2048 blocks in all beyond one per channel
+  const long long n = A * B;
+  long long per = (n + 16383) / 16384;
+  const long long cap = 2048LL / C > 1 ? 2048LL / C : 1;
+  if (per > cap) per = cap;
+  if (per < 1) per = 1;
+  (void)hipMemsetAsync(stats, 0, (size_t)3 * C * sizeof(unsigned), s);
+  hipLaunchKernelGGL(k_channel_stats, dim3(C, (unsigned)per), dim3(256), 0, s, x, A, C, B, stats);
   const long long nout = outer * Lo;
-  hipLaunchKernelGGL(k_channel_quant, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, s, x, y, nout, L, Lo, C,
+  long long nblk = (nout + 255) / 256;
+  if (nblk > (1LL << 20)) nblk = 1LL << 20;
+  if (nblk < 1) nblk = 1;
+  hipLaunchKernelGGL(k_channel_quant, dim3((unsigned)nblk), dim3(256), 0, s, x, y, nout, L, Lo, C,
                      stats, bits, scheme);
 }
 

@@ -18,6 +18,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/util/Exception.h>
 
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -49,6 +50,11 @@ at::Tensor workspace(size_t nbytes, const at::Tensor& like) {
   return at::empty({static_cast<int64_t>(std::max<size_t>(nbytes, 256))}, like.options().dtype(at::kByte));
 }
 
+// Calls whose internal fault was repaired by a re-run (check_fault), process-wide:
+// admmq::fault_repairs (expected 0 on an undisturbed device)
+std::atomic<int64_t> g_fault_repairs{0};
+int64_t fault_repairs(bool reset) { return reset ? g_fault_repairs.exchange(0) : g_fault_repairs.load(); }
+
 // --- admm_iteration_batched -------------------------------------------------------
 // solve: -1 = the process default (admmq_set_solve_mode; fp32 unless changed), else
 // ADMMQ_SOLVE_FP32 / ADMMQ_SOLVE_SPLIT for this call.
@@ -57,7 +63,9 @@ at::Tensor workspace(size_t nbytes, const at::Tensor& like) {
 // blocks were not all resident), the call restores U and re-runs with the separate
 // finalize launch, so it never returns unfinalized factors (same results as an
 // undisturbed run). check_fault = false: no sync; the caller must check info[:, 3]
-// itself and repeat the call (with U restored) where it is nonzero.
+// itself and repeat the call (with U restored) where it is nonzero. The returned info is
+// [n, 5]: the C-ABI's {iterations run, converged, spd_error, internal fault} plus the
+// re-runs this call made (0, or 1 after a repaired fault; also counted in fault_repairs).
 std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> admm_batched_cuda(
     at::TensorList H, at::TensorList U, at::TensorList F, at::TensorList G, int64_t max_iter, double eps,
     int64_t bits, int64_t qscheme, int64_t num_attempts, bool check_spd, bool debug, int64_t solve,
@@ -100,7 +108,8 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
   const size_t nb = admmq_admm_workspace_size_ex(probs.data(), nn, na, &opt);
   TORCH_CHECK(nb != 0, "admmq: admm workspace planning failed: ", admmq_last_error());
   at::Tensor ws = workspace(nb, ref);
-  at::Tensor info = at::zeros({nn, 4}, ref.options().dtype(at::kInt));
+  at::Tensor info5 = at::zeros({nn, 5}, ref.options().dtype(at::kInt));
+  at::Tensor info = at::zeros({nn, 4}, ref.options().dtype(at::kInt));   // the C-ABI's int32[nprob * 4]
   check_rc(admmq_admm_prepare_ex(probs.data(), nn, na, &opt, ws.data_ptr(), ws.numel(), stream), "admm_prepare");
   if (check_spd || max_iter <= 1) {
     // source/admm.py:54 raises before anything is modified: one sync per call
@@ -111,10 +120,15 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
                        "linalg.cholesky: The factorization could not be completed because the input is not "
                        "positive-definite.");
   }
+  auto info_out = [&](int64_t reruns) {
+    info5.narrow(1, 0, 4).copy_(info);
+    if (reruns) info5.select(1, 4).fill_(reruns);
+    return info5;
+  };
   if (max_iter <= 1) {   // the reference returns H unchanged (the Python drop-in returns the caller's object)
     std::vector<at::Tensor> same;
     for (const at::Tensor& h : H) same.push_back(h.clone());
-    return {same, info, hts, xs};
+    return {same, info_out(0), hts, xs};
   }
   std::vector<at::Tensor> ubak;   // U before the run: restored if the run must be repeated
   if (check_fault)
@@ -126,16 +140,19 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
              "admm_run");
   };
   run();
+  int64_t reruns = 0;
   if (check_fault && info.select(1, 3).max().item<int32_t>() != 0) {   // internal fault: repeat without the fused finalize
     for (size_t i = 0; i < n; ++i) Uc[i].copy_(ubak[i]);
     opt.fused_finalize = 0;
     check_rc(admmq_admm_prepare_ex(probs.data(), nn, na, &opt, ws.data_ptr(), ws.numel(), stream), "admm_prepare");
     run();
     TORCH_CHECK(info.select(1, 3).max().item<int32_t>() == 0, "admmq: internal fault in the separate-finalize re-run");
+    reruns = 1;
+    g_fault_repairs.fetch_add(1);
   }
   for (size_t i = 0; i < n; ++i)   // U is updated in place (source/admm.py:60)
     if (!U[i].is_same(Uc[i])) const_cast<at::Tensor&>(U[i]).copy_(Uc[i]);
-  return {outs, info, hts, xs};
+  return {outs, info_out(reruns), hts, xs};
 }
 
 std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> admm_batched_meta(
@@ -148,7 +165,7 @@ std::tuple<std::vector<at::Tensor>, at::Tensor, std::vector<at::Tensor>, std::ve
     if (debug) { hts.push_back(at::empty_like(h)); xs.push_back(at::empty_like(h)); }
   }
   const int64_t n = static_cast<int64_t>(H.size());
-  return {outs, at::empty({n, 4}, H[0].options().dtype(at::kInt)), hts, xs};
+  return {outs, at::empty({n, 5}, H[0].options().dtype(at::kInt)), hts, xs};
 }
 
 // --- quantize_batched ----------------------------------------------------------------
@@ -332,6 +349,7 @@ TORCH_LIBRARY(admmq, m) {
   m.def("quantize_channel(Tensor x, int bits, int qscheme, int dim) -> Tensor");
   m.def("cp_gram_mttkrp(Tensor[] W, Tensor[] factors, int mode) -> (Tensor[] G, Tensor[] F)");
   m.def("cp_rel_error(Tensor[] W, Tensor[] factors) -> Tensor");
+  m.def("fault_repairs(bool reset=False) -> int", &fault_repairs);
 }
 
 TORCH_LIBRARY_IMPL(admmq, CUDA, m) {

@@ -374,6 +374,8 @@ def emulate_shards(a):
     from admmq import _lib
     lib = _lib.load()
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
+    _lib.check(lib.admmq_debug_set_ksplit(a.ksplit), "ksplit")
+    _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
     N = a.emulate_world
     full, _, _ = build_workload(a.model, 0, 1, "layers", device)
     full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
@@ -423,6 +425,12 @@ def main():
                          "per-problem tile rows (-1: library default)")
     ap.add_argument("--f32-tiles", type=int, default=3, help="A/B: tile-row rule 0..3 of --f32-kernel 1 / 2")
     ap.add_argument("--gemm-ks", type=int, default=1, help="A/B: fp32 64x64 tiles with 4 (1) or 8 (2) waves")
+    ap.add_argument("--ksplit", type=int, default=1, choices=[0, 1],
+                    help="A/B: K-split of the fp32 solve tiles of factors too small to fill the chip (1, default: "
+                         "pieces fixed by each factor's shape) or never (0)")
+    ap.add_argument("--ksplit-form", type=int, default=1, choices=[0, 1, 2],
+                    help="A/B: K-split pieces run in parallel where the launch leaves CUs idle (1, default), always "
+                         "serially in one workgroup (0) or always in parallel (2); same bits")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
@@ -444,6 +452,8 @@ def main():
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
     _lib.check(lib.admmq_debug_set_search_units_per_block(a.search_units), "search_units_per_block")
     _lib.check(lib.admmq_debug_set_gemm_ks(a.gemm_ks), "gemm_ks")
+    _lib.check(lib.admmq_debug_set_ksplit(a.ksplit), "ksplit")
+    _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
     if a.f32_kernel >= 0:
         _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")
     split = a.solve == "split"

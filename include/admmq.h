@@ -72,8 +72,12 @@ int32_t admmq_admm_prepare(const admmq_problem* probs, int32_t nprob, int32_t nu
  * dual update, residual test} per problem, with the per-problem early exit when
  * r < eps and s < eps. Writes H_out and U. info (device int32[nprob*4], may be
  * NULL) receives {iterations run, converged, spd_error, internal fault} per problem
- * (internal fault: see admmq_admm_run_ex). Uses the solve mode its prepare recorded;
- * ADMMQ_ERR_ARG for a workspace no prepare has set up. */
+ * (internal fault: see admmq_admm_run_ex). With info == NULL the run never takes the
+ * fused paths that can report an internal fault (as fused_finalize = 0), so a NULL-info
+ * call always returns finalized results. Uses the solve mode its prepare recorded;
+ * ADMMQ_ERR_ARG for a workspace no prepare has set up, or whose prepare planned other
+ * problems or another buffer layout (the record is kept per workspace address: prepare
+ * again after reallocating a workspace). */
 int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
                        int32_t qscheme, int32_t num_attempts, void* workspace, size_t workspace_bytes,
                        int32_t* info, void* stream);
@@ -101,7 +105,8 @@ int32_t admmq_admm_prepare_ex(const admmq_problem* probs, int32_t nprob, int32_t
  * its job's selection timed out because the search launch's blocks were not all resident,
  * e.g. other work on the device). The affected elements were NOT finalized: H_out / U of
  * that call are invalid and the caller must restore U and re-run with fused_finalize = 0
- * (the PyTorch op does this itself). */
+ * (the PyTorch op does this itself). info == NULL: fused_finalize is treated as 0 (no
+ * fused path runs, so no fault can go unreported). */
 int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max_iter, float eps, int32_t bits,
                           int32_t qscheme, int32_t num_attempts, const admmq_admm_options* opt, void* workspace,
                           size_t workspace_bytes, int32_t* info, void* stream);

@@ -131,3 +131,16 @@ def test_als_contractions_refuse_cpu_tensors():
         gram_mttkrp(W, fs, 0)
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         rel_error(W, fs)
+
+
+def test_ksplit_pieces_by_shape(lib):
+    """K-split pieces of the fp32 solve tiles (api.hip ksplit_pieces) depend on (I, R)
+    only: the resnet18 layer4 conv modes (512, 1141) take 3 pieces of 12 K-steps, the
+    (512, 759) ones 2, the mid layers 2-4, factors whose tiles fill the chip (C5, resnet50
+    (2048, 204)), 32-row and thin factors, and short K ranges none."""
+    expect = {(512, 1141): 3, (512, 759): 2, (256, 759): 4, (256, 566): 3, (256, 375): 2, (128, 375): 2,
+              (128, 278): 1, (64, 134): 1, (4096, 1024): 1, (11008, 1492): 1, (2048, 204): 1, (32, 1141): 1,
+              (9, 1141): 1, (1024, 1141): 1}
+    for (I, R), n in expect.items():
+        assert lib.admmq_debug_ksplit_pieces(I, R) == n, (I, R, lib.admmq_debug_ksplit_pieces(I, R))
+    assert lib.admmq_debug_ksplit_pieces(0, 5) == 0

@@ -280,3 +280,55 @@ def test_fp32_staging_forms_equal(torch_dev):
                     assert torch.equal(h0, h1) and torch.equal(u0, u1)
     finally:
         _lib.check(lib.admmq_debug_set_gemm_stage(3), "gemm_stage")
+
+
+def test_ksplit_factors(torch_dev):
+    """K-split solve tiles (api.hip ksplit_pieces: the pieces are fixed by the factor's
+    shape; gemm_kernels.hip: run in parallel by np workgroups with the ksplit_combine
+    hand-off, or folded serially by one workgroup - the same float32 sums): the lone
+    layer4 conv factor (512, 1141) -> 3 pieces, (512, 759) -> 2, (256, 759) -> 4,
+    (256, 566) -> 3. For each: H_T within 1e-5 of the oracle (source/admm.py:56, scipy
+    float32 Cholesky) and within 1e-6 of the unsplit solve; the projection bit-exact on
+    the kernel's own X; over 4 inner iterations the parallel form (twice: the piece that
+    completes a tile varies from run to run, the piece-order sum does not), the serial
+    form and the launch's own choice bit-identical."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    lib = _lib.load()
+    expect = {(512, 1141): 3, (512, 759): 2, (256, 759): 4, (256, 566): 3}
+    for (I, R), np_ in expect.items():
+        assert lib.admmq_debug_ksplit_pieces(I, R) == np_, (I, R)
+    rng = np.random.default_rng(3)
+    probs = []
+    for (I, R) in expect:
+        B = rng.standard_normal((R, 2 * R)).astype(np.float32) / np.float32(np.sqrt(2 * R))
+        G = (B @ B.T + 0.5 * np.eye(R)).astype(np.float32)
+        probs.append((f"{I}x{R}", rng.standard_normal((I, R)).astype(np.float32),
+                      rng.standard_normal((I, R)).astype(np.float32), G))
+    worst = _check_step(torch, dev, probs, "fp32", _oracle_ht)
+    args = lambda: [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))  # noqa
+                    for (_, H, F, G) in probs]
+
+    def run(iters, debug=False):
+        ps = args()
+        Hs, dbg = admm_iteration_batched(ps, iters, 0.0, 4, MSE, debug_outputs=True)
+        return [h.cpu() for h in Hs] + [p[1].cpu() for p in ps], [d[0].cpu() for d in dbg]
+
+    try:
+        outs = []
+        for form in (2, 2, 0, 1):   # parallel, parallel, serial, launch's choice
+            _lib.check(lib.admmq_debug_set_ksplit_form(form), "ksplit_form")
+            outs.append(run(4)[0])
+        for o in outs[1:]:
+            for a, b in zip(outs[0], o):
+                assert torch.equal(a, b)
+        _lib.check(lib.admmq_debug_set_ksplit_form(1), "ksplit_form")
+        _, ht1 = run(2)   # one step, split vs unsplit: the same H_T up to the fp32 summation order
+        _lib.check(lib.admmq_debug_set_ksplit(0), "ksplit")
+        _, ht0 = run(2)
+        for (name, *_), a, b in zip(probs, ht1, ht0):
+            assert _rel(a.numpy(), b.numpy()) < 1e-6, name
+    finally:
+        _lib.check(lib.admmq_debug_set_ksplit(1), "ksplit")
+        _lib.check(lib.admmq_debug_set_ksplit_form(1), "ksplit_form")
+    print(f"K-split factors: worst H_T rel {worst:.2e}")

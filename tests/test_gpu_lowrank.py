@@ -143,3 +143,24 @@ def test_device_break_and_large_stream(env):
     # eps large: the device test breaks after the first iteration and later ones are no-ops
     _, _, it = admm_iteration(H, torch.zeros_like(H), W, H2, qf, max_iter=40, eps=1e9, return_iters=True)
     assert it == 1
+
+
+def test_krylov_projector_rank_above_block():
+    """KrylovProjector with rank > block (48 > 32): its blocks widen to the rank, so the
+    first Rayleigh-Ritz check holds r distinct Ritz pairs (a 32-wide block used to index past
+    them and repeat the top singular triplets). Equals the exact float64 truncation
+    (scripts/factorize_lowrank.py:80-82) to 1e-6 on a matrix with a decaying spectrum."""
+    import torch
+    from admmq.lowrank import KrylovProjector
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(4)
+    m, n, r = 320, 256, 48
+    Uo = torch.linalg.qr(torch.randn(m, n, generator=g, dtype=torch.float64))[0]
+    Vo = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))[0]
+    s = 0.9 ** torch.arange(n, dtype=torch.float64)
+    X = ((Uo * s) @ Vo.T).float()
+    Ue, Se, Vte = torch.linalg.svd(X.double(), full_matrices=False)
+    exact = (Ue[:, :r] * Se[:r]) @ Vte[:r]
+    P = KrylovProjector(r, block=32, seed=1)
+    got = P(X.to(dev)).double().cpu()
+    assert float(torch.linalg.norm(got - exact) / torch.linalg.norm(exact)) < 1e-6

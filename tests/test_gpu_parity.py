@@ -588,6 +588,42 @@ def test_fused_finalize_timeout_reported_and_repaired(torch_dev):
             assert _bits_equal(pr[1].cpu().numpy(), p[1].cpu().numpy())
 
 
+def test_als_sweep_fault_repair(torch_dev):
+    """admmq.factorize.als_sweep reads the internal-fault column with the SPD flags once
+    per sweep (its calls do not sync each): a fused-path fault (forced: one poll) makes it
+    restore the sweep's start and run the whole sweep again without the fused paths. The
+    factors, duals, quantized factors and losses then equal an undisturbed sweep's bit for
+    bit, and the repair is counted (_lib.fault_repairs; 0 without the fault)."""
+    torch, dev = torch_dev
+    from admmq import _lib, synthetic
+    from admmq.factorize import LayerRun, als_sweep
+    names = ["layer1.0.conv1", "layer3.1.conv2"]
+
+    def mk():
+        out = []
+        for n in names:
+            idx, spec = synthetic.find_layer("resnet18", n)
+            W = torch.from_numpy(synthetic.layer_weight(spec, idx)).to(dev)
+            g = torch.Generator().manual_seed(42)
+            out.append(LayerRun(n, W, spec.rank(), [torch.randn(k, spec.rank(), generator=g).to(dev) for k in W.shape]))
+        return out
+
+    _lib.fault_repairs(reset=True)
+    ref = mk()
+    for _ in range(2):
+        als_sweep(ref, 6, 0.0, 4, MSE)
+    assert _lib.fault_repairs() == 0
+    runs = mk()
+    als_sweep(runs, 6, 0.0, 4, MSE)
+    with _lib.fin_wait_polls(1):
+        als_sweep(runs, 6, 0.0, 4, MSE)
+    assert _lib.fault_repairs(reset=True) == 1
+    for a, b in zip(ref, runs):
+        for x, y in zip(a.factors + a.duals + a.quantized, b.factors + b.duals + b.quantized):
+            assert _bits_equal(x.cpu().numpy(), y.cpu().numpy()), a.name
+        assert a.loss == b.loss and a.lossq == b.lossq
+
+
 @pytest.mark.parametrize("route", ["ops", "cabi"])
 def test_channel_schemes_reference_kats(torch_dev, route, monkeypatch):
     """channel_symmetric / channel_affine with an explicit dim on the device

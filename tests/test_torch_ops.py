@@ -1,6 +1,6 @@
 """torch.ops.admmq.* (csrc/torch_ops.cpp over the C-ABI of include/admmq.h).
 
-CPU: the op library loads, declares the four schemas, propagates shapes on the Meta
+CPU: the op library loads, declares the six schemas, propagates shapes on the Meta
 device (fake tensors / tracing) and rejects CPU tensors in the dispatcher (there is no
 CPU kernel). GPU: every op returns exactly what the C-ABI called through ctypes
 returns, and the Python drop-ins route through the ops.
@@ -21,6 +21,7 @@ SCHEMAS = {
     "quantize_channel": "admmq::quantize_channel(Tensor x, int bits, int qscheme, int dim) -> Tensor",
     "cp_gram_mttkrp": "admmq::cp_gram_mttkrp(Tensor[] W, Tensor[] factors, int mode) -> (Tensor[] G, Tensor[] F)",
     "cp_rel_error": "admmq::cp_rel_error(Tensor[] W, Tensor[] factors) -> Tensor",
+    "fault_repairs": "admmq::fault_repairs(bool reset=False) -> int",
 }
 
 
@@ -41,7 +42,7 @@ def test_meta_shapes(ops):
     G = [torch.empty(134, 134, device=m), torch.empty(1141, 1141, device=m)]
     outs, info, hts, xs = ops.admm_iteration_batched(H, [torch.empty_like(h) for h in H], [torch.empty_like(h) for h in H],
                                                      G, 10, 1e-8, 4, 0, 200, False, True)
-    assert [o.shape for o in outs] == [h.shape for h in H] and info.shape == (2, 4) and info.dtype == torch.int32
+    assert [o.shape for o in outs] == [h.shape for h in H] and info.shape == (2, 5) and info.dtype == torch.int32
     assert [t.shape for t in hts] == [h.shape for h in H] and len(xs) == 2
     ys = ops.quantize_batched([torch.empty(3, 5, device=m)], 4, 0)
     assert ys[0].shape == (3, 5)
@@ -51,6 +52,17 @@ def test_meta_shapes(ops):
     Gs, Fs = ops.cp_gram_mttkrp(W, fs, 1)
     assert [g.shape for g in Gs] == [(7, 7), (5, 5)] and [f.shape for f in Fs] == [(32, 7), (30, 5)]
     assert ops.cp_rel_error(W, fs).shape == (2,)
+
+
+def test_fault_repair_counter(ops):
+    """The op's process-wide count of calls repaired after an internal fault (no GPU
+    needed): a non-negative int, reset to 0 by reset=True."""
+    from admmq import _lib
+    assert ops.fault_repairs(False) >= 0
+    _lib.fault_repairs(reset=True)
+    assert ops.fault_repairs(False) == 0 and _lib.fault_repairs() == 0
+    _lib.note_repair()
+    assert _lib.fault_repairs(reset=True) == 1 and _lib.fault_repairs() == 0
 
 
 def test_cpu_tensors_rejected(ops):

@@ -109,6 +109,8 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_gemm_stage": (I32, [I32]),
         "admmq_debug_set_ksplit": (I32, [I32]),
         "admmq_debug_set_ksplit_form": (I32, [I32]),
+        "admmq_debug_set_ksplit_balance": (I32, [I32, I32]),
+        "admmq_debug_ksplit_balance_count": (ctypes.c_int64, [ctypes.c_void_p, I32]),
         "admmq_debug_ksplit_pieces": (I32, [I32, I32]),
         "admmq_debug_set_even_units": (I32, [I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
@@ -142,6 +144,8 @@ def load() -> ctypes.CDLL:
         "admmq_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if name.startswith("admmq_debug_") and not hasattr(lib, name):
+            continue   # a diagnostic build (ADMMQ_LIB) from before the switch existed
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -207,6 +207,9 @@ __device__ __forceinline__ float dec_ord(unsigned e) {
 
 // Records the thread's last error text (admmq_last_error) and returns `code`.
 int set_error(int code, const char* msg);
+// Stream-ordered host -> device copy of n bytes through a pinned staging chunk (the host
+// buffer may be reused at once; the call never waits for the stream). ADMMQ_OK or an error.
+int upload_async(void* dst, const void* src, size_t n, hipStream_t s);
 
 // Host-side launchers (each defined in its own translation unit).
 void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
@@ -235,6 +238,7 @@ size_t hist_lds_bytes(int ncand, int bits);
 size_t hist3_lds_bytes(int ncand, int bits);
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_gemm_trace(unsigned long long* host, int n);
+int copy_gemm_trace2(unsigned long long* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
 int copy_fin_trace(unsigned long long* host, int n);
 int copy_small_trace(unsigned long long* host, int n);

@@ -604,7 +604,7 @@ static int run_als(const AlsPlan& pl, void* base, size_t wsb, hipStream_t s, std
   AlsUnit* dunits = reinterpret_cast<AlsUnit*>(take(nu * sizeof(AlsUnit)));
   int* dids = reinterpret_cast<int*>(take(pl.split_ids.size() * sizeof(int) + 4));
   auto up = [&](void* dst, const void* src, size_t nbytes) {
-    return nbytes == 0 || hipMemcpyAsync(dst, src, nbytes, hipMemcpyHostToDevice, s) == hipSuccess;
+    return upload_async(dst, src, nbytes, s) == ADMMQ_OK;   // pinned staging: never waits for the stream
   };
   std::vector<AlsUnit> all;
   all.reserve(nu);

@@ -35,16 +35,57 @@ static int check_hip(const char* where) {
   return ADMMQ_OK;
 }
 
-static int h2d(void* dst, const void* src, size_t n, hipStream_t s) {
+// Host -> device uploads of the plans (descriptors, tile and unit lists) through pinned
+// staging chunks, so that hipMemcpyAsync is truly asynchronous: a pageable source makes
+// the copy wait for the stream, which put every call's host planning on the GPU's
+// critical path (the host could not run ahead of the device by one mode call). A chunk
+// is reused once the event recorded after its copy has completed; one pool per device.
+struct PinnedChunk { char* p; size_t cap; hipEvent_t ev; bool used; };
+static std::mutex g_pin_mu;
+static std::vector<PinnedChunk> g_pin[64];
+static constexpr size_t kPinMaxChunks = 256;
+int upload_async(void* dst, const void* src, size_t n, hipStream_t s) {
   if (n == 0) return ADMMQ_OK;
-  // pageable source: HIP stages it before returning, so the host vector may die afterwards
-  const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  std::lock_guard<std::mutex> g(g_pin_mu);
+  std::vector<PinnedChunk>& pool = g_pin[dev];
+  PinnedChunk* c = nullptr;
+  for (PinnedChunk& k : pool)
+    if (k.cap >= n && (!k.used || hipEventQuery(k.ev) == hipSuccess)) { c = &k; break; }
+  if (!c && pool.size() >= kPinMaxChunks) {   // all busy: wait for the oldest fitting one
+    for (PinnedChunk& k : pool)
+      if (k.cap >= n) { (void)hipEventSynchronize(k.ev); c = &k; break; }
+  }
+  if (!c) {
+    PinnedChunk k;
+    k.cap = 4096;
+    while (k.cap < n) k.cap *= 2;
+    k.used = false;
+    if (hipHostMalloc(reinterpret_cast<void**>(&k.p), k.cap, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      g_err = "upload: pinned staging allocation failed";
+      return ADMMQ_ERR_HIP;
+    }
+    if (hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipHostFree(k.p);
+      g_err = "upload: event creation failed";
+      return ADMMQ_ERR_HIP;
+    }
+    pool.push_back(k);
+    c = &pool.back();
+  }
+  std::memcpy(c->p, src, n);
+  hipError_t e = hipMemcpyAsync(dst, c->p, n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev, s);
+  c->used = true;
   if (e != hipSuccess) {
     g_err = std::string("upload: ") + hipGetErrorString(e);
     return ADMMQ_ERR_HIP;
   }
   return ADMMQ_OK;
 }
+static int h2d(void* dst, const void* src, size_t n, hipStream_t s) { return upload_async(dst, src, n, s); }
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 static inline int rup(int v, int a) { return (v + a - 1) / a * a; }
@@ -124,6 +165,64 @@ static std::atomic<int> g_ksplit_par{1};
 // partial hand-off, ties to the smaller np. Only factors with fewer tiles than CUs split.
 static constexpr int kKsplitChipCUs = 256;
 static constexpr int kKsplitCost = 4;   // K-steps (~2.5 us): partial stores, arrival, sc1 reads
+// Balance (launches that fill the chip): 1 = run the pieces of the longest split tiles in
+// parallel where that lowers the launch's CU-level LPT makespan (same bits), 0 = never;
+// a parallel piece is priced kKsplitCost... g_ksplit_cost K-steps above its own.
+static std::atomic<int> g_ksplit_bal{1};
+static std::atomic<int> g_ksplit_cost{1};
+// Resident 64 x 64 fp32 solve workgroups per CU (the LPT's slots): 3 for the default 3-deep
+// staging ring (48 KB of LDS), 4 for the 2-deep ring (k_gemm_f32b<2>, 32 KB, 4 waves per SIMD)
+static int f32_slots() { return g_gemm_f32_stage == 2 ? 4 : 3; }
+// Makespan (K-steps of the busiest CU) of an LPT placement of `costs` over ncu CUs with at
+// most `slots` items each (order_tiles_for_cus' rule without its XCD tie-break); -1 when
+// the items do not fit one resident round.
+static long long lpt_makespan(std::vector<long long> costs, int ncu, int slots) {
+  if ((long long)costs.size() > (long long)ncu * slots) return -1;
+  std::sort(costs.begin(), costs.end(), std::greater<long long>());
+  // min-heap of (load, cu) over the CUs with a free slot
+  std::vector<std::pair<long long, int>> heap;
+  std::vector<int> used(ncu, 0);
+  for (int b = 0; b < ncu; ++b) heap.push_back({0, b});
+  auto cmp = [](const std::pair<long long, int>& a, const std::pair<long long, int>& b) { return a > b; };
+  std::make_heap(heap.begin(), heap.end(), cmp);
+  long long mx = 0;
+  for (long long c : costs) {
+    std::pop_heap(heap.begin(), heap.end(), cmp);
+    auto [ld, b] = heap.back();
+    heap.pop_back();
+    ld += c;
+    mx = std::max(mx, ld);
+    if (++used[b] < slots) {
+      heap.push_back({ld, b});
+      std::push_heap(heap.begin(), heap.end(), cmp);
+    }
+  }
+  return mx;
+}
+// How many of the split tiles `cand` (longest first; (nk, np)) to run as parallel pieces so
+// that the launch's LPT makespan is smallest (ties: fewer), `whole` = every tile's K-steps.
+static long long ksplit_balance(const std::vector<long long>& whole, std::vector<std::pair<int, int>> cand, int ncu,
+                                int slots, int cost) {
+  if (cand.empty() || (long long)whole.size() <= ncu) return 0;
+  std::stable_sort(cand.begin(), cand.end(), [](auto& a, auto& b) { return a.first > b.first; });
+  long long best_m = lpt_makespan(whole, ncu, slots);
+  if (best_m < 0) return 0;
+  long long best_k = 0;
+  std::vector<long long> costs = whole;
+  // remove one whole tile of each split candidate as it is split: keep a multiset by value
+  for (long long k = 1; k <= (long long)cand.size(); ++k) {
+    const int nk = cand[k - 1].first, np = cand[k - 1].second;
+    auto it = std::find(costs.begin(), costs.end(), (long long)nk);
+    if (it == costs.end()) break;
+    costs.erase(it);
+    for (int pc = 0; pc < np; ++pc) costs.push_back((pc + 1) * nk / np - pc * nk / np + cost);
+    const long long m = lpt_makespan(costs, ncu, slots);
+    if (m < 0) break;
+    if (m < best_m) { best_m = m; best_k = k; }
+  }
+  return best_k;
+}
+
 static int ksplit_pieces(int I, int R) {
   if (I <= 32) return 1;   // 32 x 64 tiles
   const int nk = rup(R, 32) / 32;
@@ -656,16 +755,35 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     whole64 += (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
   }
   pl.ksplit_par = g_ksplit_par.load() == 2 || (g_ksplit_par.load() == 1 && whole64 <= kKsplitChipCUs);
+  // A launch that fills the chip runs the pieces serially, except the `npar` longest split
+  // tiles (balance): their pieces in parallel fill the gaps a CU-level LPT of whole tiles
+  // leaves (C3 mode 0: 36-K-step tiles, max CU load 90 against a mean of 80).
+  long long npar = pl.ksplit_par ? (1LL << 40) : 0;
+  if (!pl.ksplit_par && g_ksplit_par.load() == 1 && g_ksplit_bal.load() && !pl.f32p && !pl.f32t) {
+    std::vector<long long> whole;   // K-steps of every 64 x 64 tile of the launch
+    std::vector<std::pair<int, int>> cand;   // (nk, np) of the split tiles, longest first
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
+      const long long nt = (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
+      for (long long t = 0; t < nt; ++t) whole.push_back(d.ld / 32);
+      if (d.ksplit > 1)
+        for (long long t = 0; t < nt; ++t) cand.push_back({d.ld / 32, d.ksplit});
+    }
+    npar = ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
+  }
   size_t nctr = 0;
+  long long nsplit = 0;   // split tiles emitted so far (the first npar of them run in parallel)
   for (int i : order) {
     const ProbDesc& d = pl.desc[i];
     if (pl.f32p || pl.f32t) break;
     if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;   // thin / 32-row / wide: elsewhere
     const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
-    const int nk = d.ld / 32, np = pl.ksplit_par ? d.ksplit : 1;
+    const int nk = d.ld / 32;
     for (int g0 = 0; g0 < TN; g0 += 8)
       for (int tm = 0; tm < TM; ++tm)
-        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn) {
+          const int np = (d.ksplit > 1 && nsplit++ < npar) ? d.ksplit : 1;
           for (int pc = 0; pc < np; ++pc) {   // parallel K-split pieces: [pc nk / np, (pc + 1) nk / np)
             const int k0 = pc * nk / np, k1 = (pc + 1) * nk / np;
             GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0 && pc == 0) ? 1 : 0, k1 - k0);
@@ -678,6 +796,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
             }
             pl.tiles.push_back(t);
           }
+        }
     if (d.ksplit > 1) nctr += TM * TN;
   }
   if (!pl.f32p && !pl.f32t) {
@@ -685,7 +804,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     // order as slots free up: longest first (a no-op without pieces: problems are in ld order)
     if (pl.tiles.size() > 256 * 3)
       std::stable_sort(pl.tiles.begin(), pl.tiles.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
-    order_tiles_for_cus(pl.tiles, 256, 3);
+    order_tiles_for_cus(pl.tiles, 256, f32_slots());
   }
   std::vector<GemmTile> small;
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
@@ -1105,6 +1224,32 @@ int32_t admmq_debug_set_ksplit_form(int32_t form) {
   g_ksplit_par = form;
   return ADMMQ_OK;
 }
+// diagnostics: parallel pieces for CU balance in launches that fill the chip (same bits):
+// on / off, and the price of a parallel piece in K-steps
+int32_t admmq_debug_set_ksplit_balance(int32_t on, int32_t cost) {
+  if (on < 0 || on > 1 || cost < 0 || cost > 64) return fail(ADMMQ_ERR_ARG, "ksplit balance: on 0/1, cost 0..64");
+  g_ksplit_bal = on;
+  g_ksplit_cost = cost;
+  return ADMMQ_OK;
+}
+// diagnostics: the parallel-piece count the balance picks for the 64 x 64 tiles of a batch
+// of (I, R) factors (fp32 form, default switches), or -1 on bad arguments
+int64_t admmq_debug_ksplit_balance_count(const int32_t* IR, int32_t nprob) {
+  if (!IR || nprob <= 0) return -1;
+  std::vector<long long> whole;
+  std::vector<std::pair<int, int>> cand;
+  for (int p = 0; p < nprob; ++p) {
+    const int I = IR[2 * p], R = IR[2 * p + 1];
+    if (I <= 32) continue;
+    const int ld = rup(R, 32), np = ksplit_pieces(I, R);
+    const long long nt = (long long)((I + 63) / 64) * ((ld + 63) / 64);
+    for (long long t = 0; t < nt; ++t) {
+      whole.push_back(ld / 32);
+      if (np > 1) cand.push_back({ld / 32, np});
+    }
+  }
+  return ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
+}
 // diagnostics: the K-split pieces the planner gives an (I, R) factor (0 on bad arguments)
 int32_t admmq_debug_ksplit_pieces(int32_t I, int32_t R) {
   if (I <= 0 || R <= 0) return 0;
@@ -1404,6 +1549,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 // diagnostics (not in include/admmq.h): per-block timelines of the last launches (make TRACE=1)
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
+int32_t admmq_debug_gemm_trace2(unsigned long long* host, int32_t n) { return copy_gemm_trace2(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
 int32_t admmq_debug_fin_trace(unsigned long long* host, int32_t n) { return copy_fin_trace(host, n); }
 int32_t admmq_debug_small_trace(unsigned long long* host, int32_t n) { return copy_small_trace(host, n); }

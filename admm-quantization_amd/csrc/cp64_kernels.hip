@@ -279,7 +279,7 @@ static int run_cp64(const Cp64Plan& pl, void* base, size_t wsb, hipStream_t s, s
   Cp64Unit* dunits = reinterpret_cast<Cp64Unit*>(take(pl.units.size() * sizeof(Cp64Unit)));
   int* dids = reinterpret_cast<int*>(take(pl.split_ids.size() * sizeof(int) + 4));
   auto up = [&](void* dst, const void* src, size_t nbytes) {
-    return nbytes == 0 || hipMemcpyAsync(dst, src, nbytes, hipMemcpyHostToDevice, s) == hipSuccess;
+    return upload_async(dst, src, nbytes, s) == ADMMQ_OK;   // pinned staging: never waits for the stream
   };
   if (!up(djobs, pl.jobs.data(), pl.jobs.size() * sizeof(Cp64Job)) ||
       !up(dunits, pl.units.data(), pl.units.size() * sizeof(Cp64Unit)) ||

@@ -164,6 +164,13 @@ __device__ __forceinline__ bool ksplit_combine(const GemmTile& tl, f32x16& acc, 
 // (block << 48) | (K-steps << 40) | (XCC_ID << 32) | HW_ID} (admmq_debug_gemm_trace, tools/gemm_timeline.py)
 constexpr int kGemmTraceMax = 8192;
 __device__ unsigned long long g_gemm_trace[kGemmTraceMax][4];   // + shader-clock cycles of the workgroup
+// ... and per workgroup {K-loop end, K-split combine end} (k_gemm_f32b; 0 where not reached)
+__device__ unsigned long long g_gemm_trace2[kGemmTraceMax][2];
+int copy_gemm_trace2(unsigned long long* host, int n) {
+  n = n < kGemmTraceMax ? n : kGemmTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace2), (size_t)n * 2 * sizeof(unsigned long long)) == hipSuccess
+             ? n : -1;
+}
 int copy_gemm_trace(unsigned long long* host, int n) {
   n = n < kGemmTraceMax ? n : kGemmTraceMax;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess
@@ -836,13 +843,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
 #undef ADMMQ_STEP
 #undef ADMMQ_ISSUE
   wait_vmcnt<0>();   // the refills past the end land before the workgroup ends
+  const unsigned long long TK = ADMMQ_NOW();
   if (ser > 1) {     // serial K-split: the last piece
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = psum[r] + acc[r];
   }
   if (tl.np > 1) {   // K-split piece: only the piece that completes the tile goes on
     __shared__ int klast;
-    if (!ksplit_combine(tl, acc, &klast)) return;
+    const bool go = ksplit_combine(tl, acc, &klast);
+    if (ADMMQ_TRACE && tid == 0 && blockIdx.x < kGemmTraceMax) {
+      g_gemm_trace2[blockIdx.x][0] = TK;
+      g_gemm_trace2[blockIdx.x][1] = ADMMQ_NOW();
+      if (!go) {   // a piece that did not complete its tile: {start, end, info | 1 << 63}
+        g_gemm_trace[blockIdx.x][0] = T0;
+        g_gemm_trace[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - C0;
+        g_gemm_trace[blockIdx.x][1] = ADMMQ_NOW();
+        g_gemm_trace[blockIdx.x][2] = (1ull << 63) | ((unsigned long long)blockIdx.x << 48) |
+                                      ((unsigned long long)(nk & 0xFF) << 40) |
+                                      ((unsigned long long)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFF) << 32) |
+                                      __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      }
+    }
+    if (!go) return;
+  } else if (ADMMQ_TRACE && tid == 0 && blockIdx.x < kGemmTraceMax) {
+    g_gemm_trace2[blockIdx.x][0] = TK;
+    g_gemm_trace2[blockIdx.x][1] = TK;
   }
   if constexpr (!PRE) load_u();
   unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;

@@ -107,17 +107,23 @@ __global__ __launch_bounds__(256) void k_channel_stats(const float* __restrict__
 // (C == 1 ? 0 : j) for output column j: torch broadcasts the (C,) statistics against the
 // tensor's last dimension (the host checked L == C or one of them is 1; Lo = max(L, C)).
 // Grid-stride over the outputs (the grid is capped; outputs may exceed 2^32).
+__device__ __noinline__ void channel_quant_one(const float* __restrict__ x, float* __restrict__ y, long long i, int L,
+                                               int Lo, int C, const unsigned* __restrict__ stats, int bits, int scheme) {
+  const long long o = i / Lo;
+  const int j = (int)(i - o * Lo);
+  const int ci = C == 1 ? 0 : j;
+  const float tmin = dec_ord(~stats[3 * ci + 0]), tmax = dec_ord(stats[3 * ci + 1]);
+  const QParams qp = qparams_stats(scheme, bits, tmin, tmax, (int)stats[3 * ci + 2], 0, 0.f, 0.f);
+  y[i] = apply_quant(x[o * L + (L == 1 ? 0 : j)], qp);
+}
 __global__ __launch_bounds__(256) void k_channel_quant(const float* __restrict__ x, float* __restrict__ y,
                                                        long long nout, int L, int Lo, int C,
                                                        const unsigned* __restrict__ stats, int bits, int scheme) {
   const long long step = (long long)blockDim.x * gridDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += step) {
-    const long long o = i / Lo;
-    const int j = (int)(i - o * Lo);
-    const int ci = C == 1 ? 0 : j;
-    const float tmin = dec_ord(~stats[3 * ci + 0]), tmax = dec_ord(stats[3 * ci + 1]);
-    const QParams qp = qparams_stats(scheme, bits, tmin, tmax, (int)stats[3 * ci + 2], 0, 0.f, 0.f);
-    y[i] = apply_quant(x[o * L + (L == 1 ? 0 : j)], qp);
+  for (long long i0 = (long long)blockIdx.x * blockDim.x; i0 < nout; i0 += step) {
+    const long long i = i0 + threadIdx.x;
+    if (i >= nout) break;
+    channel_quant_one(x, y, i, L, Lo, C, stats, bits, scheme);
   }
 }
 

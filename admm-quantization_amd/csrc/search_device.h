@@ -109,10 +109,14 @@ __device__ __forceinline__ void hist_insert_elem(float x, const float* thr, int 
     const bool exact = (a >= tk[b - 1]) && (a < tk[b]);
     const bool add = act && exact;
     slow |= (act && !exact) ? (1u << k) : 0u;
-    const int bin = add ? b : dummy;
-    atomicAdd(&h1[bin], add ? af : 0ull);
-    atomicAdd(&h2[bin], add ? (unsigned)(2 * k - 1) : 0u);
+    // only the lanes whose level k is active add (1-2 of the QMAX levels of an element):
+    // the masked-off lanes cost no LDS atomic (the former private dummy bins did)
+    if (add) {
+      atomicAdd(&h1[b], af);
+      atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+    }
   }
+  (void)dummy;
   if (slow) {   // rare: exact breakpoint by binary search (largest b with thr[k][b-1] <= a)
 #pragma unroll 1
     for (int k = 1; k <= QMAX; ++k) {

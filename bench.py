@@ -66,6 +66,32 @@ def workload_name(model, work, max_iter_admm):
             f"{max_iter_admm - 1} ADMM iters (eps=0), 4-bit mse-minmax, rate 2.0")
 
 
+def _model_specs(model):
+    from admmq import synthetic
+    return synthetic.MODELS[model]()
+
+
+SHARD_MODEL_FILE = os.path.join(ROOT, "profiles", "r04_shard_model.json")
+
+
+def measured_cap(model, loads, total):
+    """Shard sweep time priced by MEASURED per-sweep time instead of flops: the affine model
+    T(shard) = T0 + kappa * cost (cost = the LPT flop model's load) fitted to emulated
+    shard timings of this model (tools/fit_shard_model.py -> profiles/r04_shard_model.json;
+    T0 is the per-sweep latency floor every shard pays - the thin loop and each inner
+    iteration's kernel chain - which the flop model ignores). Returns the implied strong-
+    scaling cap T(whole model) / max T(shard) and the fit, or None without a fit."""
+    try:
+        with open(SHARD_MODEL_FILE) as f:
+            fit = json.load(f)[model]
+    except (OSError, ValueError, KeyError):
+        return None
+    t = lambda c: fit["t0_ms"] + fit["kappa_ms_per_cost"] * c  # noqa: E731
+    return {"measured_speedup_cap": t(total) / max(t(c) for c in loads),
+            "shard_model": {"t0_ms": fit["t0_ms"], "kappa_ms_per_cost": fit["kappa_ms_per_cost"],
+                            "source": os.path.relpath(SHARD_MODEL_FILE, ROOT), "fit_max_rel_err": fit["max_rel_err"]}}
+
+
 def build_workload(model, rank, world, shard, device):
     """This rank's layers (LPT over layer cost when sharding), their
     synthetic weights and seed-42 random init, plus the static shard plan: every rank's
@@ -97,6 +123,9 @@ def build_workload(model, rank, world, shard, device):
                 "layers_per_rank": [sum(1 for i in owner if owner[i] == k) for k in range(world)],
                 "lpt_speedup_cap": total / max(loads),
                 "whole_layer_speedup_cap": total / max(layer_cost(s, s.rank()) for s in specs)}
+        mc = measured_cap(model, loads, total)
+        if mc:
+            info.update(mc)
     return work, numel, info
 
 
@@ -376,13 +405,15 @@ def emulate_shards(a):
     _lib.check(lib.admmq_set_solve_mode(0 if a.solve == "fp32" else 1), "set_solve_mode")
     _lib.check(lib.admmq_debug_set_ksplit(a.ksplit), "ksplit")
     _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
+    _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
     N = a.emulate_world
     full, _, _ = build_workload(a.model, 0, 1, "layers", device)
     full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
     del full
-    shard_ms, nlayers, info, shard_us = [], [], None, []
+    shard_ms, nlayers, info, shard_us, shard_cost = [], [], None, [], []
     for r in range(N):
         work, _, info = build_workload(a.model, r, N, "layers", device)
+        shard_cost.append(sum(layer_cost(s, R) for (s, _, R, _) in work))
         nlayers.append(len(work))
         shard_ms.append(time_steps(work, a.max_iter_admm, a.steps, a.warmup) if work else 0.0)
         shard_us.append(class_avgs(work, a.max_iter_admm) if work else {})
@@ -391,6 +422,7 @@ def emulate_shards(a):
     out = {"metric": "emulated layer-shard sweep time (one GPU)", "model": a.model, "world": N, "solve": a.solve,
            "max_iter_admm": a.max_iter_admm, "steps": a.steps, "full_ms_per_sweep": full_ms,
            "shard_ms_per_sweep": shard_ms, "layers_per_rank": nlayers, "busiest_ms": max(shard_ms),
+           "shard_cost": shard_cost, "total_cost": sum(layer_cost(s, s.rank()) for s in _model_specs(a.model)),
            "shard_kernel_avg_us": shard_us,
            "implied_speedup": full_ms / max(shard_ms), "lpt_speedup_cap": info["lpt_speedup_cap"],
            "whole_layer_speedup_cap": info["whole_layer_speedup_cap"], "policy": info["policy"]}
@@ -431,6 +463,11 @@ def main():
     ap.add_argument("--ksplit-form", type=int, default=1, choices=[0, 1, 2],
                     help="A/B: K-split pieces run in parallel where the launch leaves CUs idle (1, default), always "
                          "serially in one workgroup (0) or always in parallel (2); same bits")
+    ap.add_argument("--ksplit-bal", default="1:1",
+                    help="A/B: ON:COST - run the pieces of the longest split tiles in parallel where that lowers "
+                         "the launch's CU-level LPT makespan (a parallel piece priced COST K-steps extra); same bits")
+    ap.add_argument("--gemm-stage", type=int, default=-1,
+                    help="A/B: fp32 64x64 staging form 0..4 (library default 3; 2 = 2-deep ring, 4 tiles per CU)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
@@ -454,6 +491,9 @@ def main():
     _lib.check(lib.admmq_debug_set_gemm_ks(a.gemm_ks), "gemm_ks")
     _lib.check(lib.admmq_debug_set_ksplit(a.ksplit), "ksplit")
     _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
+    _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
+    if a.gemm_stage >= 0:
+        _lib.check(lib.admmq_debug_set_gemm_stage(a.gemm_stage), "gemm_stage")
     if a.f32_kernel >= 0:
         _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")
     split = a.solve == "split"
@@ -464,6 +504,7 @@ def main():
         gather_factors(run_step(work, a.max_iter_admm), rank, world, numel, device)
     torch.cuda.synchronize()
 
+    _lib.fault_repairs(reset=True)   # fused-path faults repaired by a re-run inside the timed steps (expected 0)
     prof = not a.no_profile
     if prof:
         n_launch = a.steps * 3 * 6 * (a.max_iter_admm // a.prof_every + 1) + 64
@@ -487,6 +528,7 @@ def main():
         _lib.check(lib.admmq_profile_end(ms, cnt), "profile_end")
         kern = {"ms": list(ms), "launches": list(cnt)}
 
+    repairs = _lib.fault_repairs()
     elapsed_max, total_fi = reduce_over_ranks(elapsed, fi_per_step * a.steps, world, device)
 
     if rank == 0:
@@ -502,6 +544,7 @@ def main():
                           "mse_search": "exhaustive" if a.exhaustive else "two-stage exact",
                           "solve": a.solve}}
         out["step_roofline"] = step_roofline(work, a.max_iter_admm, out["ms_per_step"])
+        out["finalize_repairs"] = repairs   # rank 0's calls re-run after a fused-path internal fault
         if shard_info:
             out["config"]["shard"] = shard_info
         if kern is not None:

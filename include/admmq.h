@@ -4,7 +4,10 @@
  * Every entry point is stream-ordered on the caller's HIP stream (`stream` is a
  * hipStream_t passed as void*), takes plain device pointers to row-major float32
  * buffers, uses only caller-owned workspace, and returns an int32 status
- * (ADMMQ_OK = 0). No entry point allocates, frees or synchronises.
+ * (ADMMQ_OK = 0). No entry point allocates device memory or synchronises with the
+ * device: plans (descriptor and work-unit tables) go up with hipMemcpyAsync from a pool
+ * of pinned host staging chunks the library grows on first use and reuses once their
+ * copies have completed, so a call returns while its launches are still queued.
  *
  * Reference interfaces replaced (KamikaziZen/admm-quantization @ 2024_10_08):
  *   admmq_admm_prepare + admmq_admm_run  <- source/admm.py:51-67  admm_iteration(H,U,F,G,max_iter,eps,bits,qscheme)

@@ -120,3 +120,19 @@ def test_f9_channel_kats():
         assert _sha(y) == case["sha"], case["id"]
         ref = arrays[case["id"]]
         assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
+
+
+def test_f10_lowrank_fixture_consistent():
+    """F10 (reference quant + low-rank loop, 30 outer iterations, five runs): the band holds
+    the reference's own history, its runs agree to 1e-3 for 4 outer iterations, and every
+    run keeps rel above 1 (the reference's behaviour on this random-init synthetic input)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "f10_lowrank.json")) as f:
+        ref = json.load(f)
+    h, lo, hi = ref["rel_history"], ref["band_min"], ref["band_max"]
+    assert len(h) == len(lo) == len(hi) == ref["outer"] == 30
+    assert all(a <= x <= b for a, x, b in zip(lo, h, hi))
+    assert all(b - a < 1e-3 for a, b in zip(lo[:4], hi[:4]))
+    for run in [h] + [v["rel_history"] for v in ref["perturbed"].values()]:
+        assert min(run) > 1.0

@@ -49,7 +49,7 @@ for b in range(got):
         clk.append(buf[4 * b + 3] / ((t1 - t0) / 100.0) / 1e3)   # shader cycles per us -> GHz
     if t0 == 0 or t1 < t0:
         break
-    wg = hid >> 48
+    wg = (hid >> 48) & 0x7FFF
     nk = (hid >> 40) & 0xFF
     xcc = (hid >> 32) & 0xFF
     hw = hid & 0xFFFFFFFF
@@ -57,6 +57,19 @@ for b in range(got):
     sh = (hw >> 12) & 1
     se = (hw >> 13) & 0x7
     recs.append((b, t0, t1, xcc, se, sh, cu, wg, nk))
+# K-split phases (k_gemm_f32b, TRACE builds): K-loop end and combine end per workgroup
+buf2 = (ctypes.c_ulonglong * (2 * n))()
+lib.admmq_debug_gemm_trace2.restype = ctypes.c_int32
+if lib.admmq_debug_gemm_trace2(buf2, n) > 0:
+    ph = collections.defaultdict(list)
+    for (b, s0, s1, *_r) in recs:
+        tk, tc = buf2[2 * b], buf2[2 * b + 1]
+        if tk >= s0 and tc >= tk and s1 >= tc and tk:
+            done = "last/whole" if not (buf[4 * b + 2] >> 63) else "non-last piece"
+            ph[done].append(((tk - s0) / 100, (tc - tk) / 100, (s1 - tc) / 100))
+    for k, v in ph.items():
+        m = [sum(x[i] for x in v) / len(v) for i in range(3)]
+        print(f"{k}: n {len(v)}  K-loop {m[0]:.2f}  combine {m[1]:.2f}  epilogue {m[2]:.2f} us (means)")
 t0 = min(r[1] for r in recs)
 t1 = max(r[2] for r in recs)
 print(f"tiles {len(recs)}  span {(t1 - t0) / 100:.2f} us (100 MHz ticks)")

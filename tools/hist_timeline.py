@@ -18,13 +18,14 @@ from admmq.admm import admm_iteration_batched  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--iters", type=int, default=4)
+ap.add_argument("--shapes", default="", help="I:R,I:R,... instead of the resnet18 factors of --mode")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 g = torch.Generator().manual_seed(0)
 probs = []
-for s in synthetic.resnet18_layers():
-    R = s.rank()
-    I = s.shape[a.mode]
+shapes = ([tuple(int(v) for v in x.split(":")) for x in a.shapes.split(",")] if a.shapes else
+          [(s.shape[a.mode], s.rank()) for s in synthetic.resnet18_layers()])
+for I, R in shapes:
     B = torch.randn(R, 2 * R, generator=g) / (2 * R) ** 0.5
     G = (B @ B.T + 0.5 * torch.eye(R)).to(dev)
     F = torch.randn(I, R, generator=g).to(dev)

@@ -220,7 +220,7 @@ void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits,
                        float eps, int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0 = nullptr,
-                 hipEvent_t ev1 = nullptr);
+                 hipEvent_t ev1 = nullptr, bool prefetch_u = false);
 extern int g_gemm_ks_f32;
 extern int g_gemm_f32_stage;   // fp32 64 x 64 staging form (gemm_kernels.hip)
 void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,

@@ -578,6 +578,87 @@ static bool plan_thin_teams(AdmmPlan& pl, int ncu) {
   return true;
 }
 
+// The fp32 64 x 64 tile list of a plan (pl.desc, pl.split set; not f32p / f32t): whole
+// tiles in problem order (XCD-aware within each problem), K-split pieces in parallel or
+// folded serially, then the CU-level LPT order. part / ctr are left for the caller.
+template <class WideFn>
+static void build_big_tiles(AdmmPlan& pl, const std::vector<int>& order, WideFn wide_prob) {
+  pl.tiles.clear();
+  // The K-split pieces of a factor (fixed by its shape) run in parallel, np workgroups per
+  // tile, only in a launch whose whole tiles leave CUs idle (a lone large factor, as in a
+  // multi-GPU shard); otherwise one workgroup folds them serially (same bits, no hand-off).
+  long long whole64 = 0;
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
+    whole64 += (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
+  }
+  pl.ksplit_par = g_ksplit_par.load() == 2 || (g_ksplit_par.load() == 1 && whole64 <= kKsplitChipCUs);
+  // A launch that fills the chip runs the pieces serially, except the `npar` longest split
+  // tiles (balance): their pieces in parallel fill the gaps a CU-level LPT of whole tiles
+  // leaves (C3 mode 0: 36-K-step tiles, max CU load 90 against a mean of 80).
+  long long npar = pl.ksplit_par ? (1LL << 40) : 0;
+  if (!pl.ksplit_par && g_ksplit_par.load() == 1 && g_ksplit_bal.load()) {
+    std::vector<long long> whole;   // K-steps of every 64 x 64 tile of the launch
+    std::vector<std::pair<int, int>> cand;   // (nk, np) of the split tiles, longest first
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
+      const long long nt = (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
+      for (long long t = 0; t < nt; ++t) whole.push_back(d.ld / 32);
+      if (d.ksplit > 1)
+        for (long long t = 0; t < nt; ++t) cand.push_back({d.ld / 32, d.ksplit});
+    }
+    npar = ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
+  }
+  long long nsplit = 0;   // split tiles emitted so far (the first npar of them run in parallel)
+  for (int i : order) {
+    const ProbDesc& d = pl.desc[i];
+    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;   // thin / 32-row / wide: elsewhere
+    const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
+    const int nk = d.ld / 32;
+    for (int g0 = 0; g0 < TN; g0 += 8)
+      for (int tm = 0; tm < TM; ++tm)
+        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn) {
+          const int np = (d.ksplit > 1 && nsplit++ < npar) ? d.ksplit : 1;
+          for (int pc = 0; pc < np; ++pc) {   // parallel K-split pieces: [pc nk / np, (pc + 1) nk / np)
+            const int k0 = pc * nk / np, k1 = (pc + 1) * nk / np;
+            GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0 && pc == 0) ? 1 : 0, k1 - k0);
+            if (np > 1) {
+              t.k0 = k0; t.np = np; t.pc = pc;   // (part / ctr: filled per call)
+            } else {
+              t.ser = d.ksplit;   // serial form (1: no K-split)
+            }
+            pl.tiles.push_back(t);
+          }
+        }
+  }
+  {
+    // a launch of more tiles than resident slots (K-split pieces, C4) is dispatched in
+    // order as slots free up: longest first (a no-op without pieces: problems are in ld order)
+    if (pl.tiles.size() > 256 * 3)
+      std::stable_sort(pl.tiles.begin(), pl.tiles.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
+    order_tiles_for_cus(pl.tiles, 256, f32_slots());
+  }
+}
+
+// Memo of build_big_tiles by a hash of its inputs (bounded; cleared when full)
+static std::mutex g_tile_mu;
+static std::unordered_map<unsigned long long, std::pair<std::vector<GemmTile>, bool>> g_tile_cache;
+static bool tile_cache_get(unsigned long long key, std::vector<GemmTile>& tiles, bool& par) {
+  std::lock_guard<std::mutex> g(g_tile_mu);
+  auto it = g_tile_cache.find(key);
+  if (it == g_tile_cache.end()) return false;
+  tiles.insert(tiles.end(), it->second.first.begin(), it->second.first.end());
+  par = it->second.second;
+  return true;
+}
+static void tile_cache_put(unsigned long long key, const std::vector<GemmTile>& tiles, bool par) {
+  std::lock_guard<std::mutex> g(g_tile_mu);
+  if (g_tile_cache.size() >= 64) g_tile_cache.clear();
+  g_tile_cache[key] = {tiles, par};
+}
+
 static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws, AdmmPlan& pl, int solve_mode) {
   if (nprob <= 0 || !probs) return fail(ADMMQ_ERR_ARG, "no problems");
   if (ncand < 1) return fail(ADMMQ_ERR_ARG, "num_attempts must be >= 1");
@@ -745,66 +826,40 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   for (int i = 0; i < nprob; ++i)
     if (pl.desc[i].ksplit > 1) pl.nkctr += (size_t)(pl.desc[i].Ip / 64) * ((pl.desc[i].ld + 63) / 64);
   pl.d_kctr = cv.take<unsigned>(std::max<size_t>(pl.nkctr, 1));
-  // The K-split pieces of a factor (fixed by its shape) run in parallel, np workgroups per
-  // tile, only in a launch whose whole tiles leave CUs idle (a lone large factor, as in a
-  // multi-GPU shard); otherwise one workgroup folds them serially (same bits, no hand-off).
-  long long whole64 = 0;
-  for (int i : order) {
-    const ProbDesc& d = pl.desc[i];
-    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
-    whole64 += (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
-  }
-  pl.ksplit_par = g_ksplit_par.load() == 2 || (g_ksplit_par.load() == 1 && whole64 <= kKsplitChipCUs);
-  // A launch that fills the chip runs the pieces serially, except the `npar` longest split
-  // tiles (balance): their pieces in parallel fill the gaps a CU-level LPT of whole tiles
-  // leaves (C3 mode 0: 36-K-step tiles, max CU load 90 against a mean of 80).
-  long long npar = pl.ksplit_par ? (1LL << 40) : 0;
-  if (!pl.ksplit_par && g_ksplit_par.load() == 1 && g_ksplit_bal.load() && !pl.f32p && !pl.f32t) {
-    std::vector<long long> whole;   // K-steps of every 64 x 64 tile of the launch
-    std::vector<std::pair<int, int>> cand;   // (nk, np) of the split tiles, longest first
+  // The 64 x 64 tile list (pieces, serial folds, CU order) is a pure function of the
+  // problems' shapes and the switches: memoised, so repeated calls (prepare and run of one
+  // call, every ALS sweep) skip the LPT placement; the per-call pointers are filled after.
+  std::vector<size_t> ctrbase(nprob, 0);
+  {
+    size_t n = 0;
     for (int i : order) {
       const ProbDesc& d = pl.desc[i];
-      if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;
-      const long long nt = (long long)(d.Ip / 64) * ((d.ld + 63) / 64);
-      for (long long t = 0; t < nt; ++t) whole.push_back(d.ld / 32);
-      if (d.ksplit > 1)
-        for (long long t = 0; t < nt; ++t) cand.push_back({d.ld / 32, d.ksplit});
+      if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d) || d.ksplit <= 1) continue;
+      ctrbase[i] = n;
+      n += (size_t)(d.Ip / 64) * ((d.ld + 63) / 64);
     }
-    npar = ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
-  }
-  size_t nctr = 0;
-  long long nsplit = 0;   // split tiles emitted so far (the first npar of them run in parallel)
-  for (int i : order) {
-    const ProbDesc& d = pl.desc[i];
-    if (pl.f32p || pl.f32t) break;
-    if (d.I <= kThinRows || d.Ip == 32 || wide_prob(d)) continue;   // thin / 32-row / wide: elsewhere
-    const int TM = d.Ip / 64, TN = (d.ld + 63) / 64;
-    const int nk = d.ld / 32;
-    for (int g0 = 0; g0 < TN; g0 += 8)
-      for (int tm = 0; tm < TM; ++tm)
-        for (int tn = g0; tn < std::min(TN, g0 + 8); ++tn) {
-          const int np = (d.ksplit > 1 && nsplit++ < npar) ? d.ksplit : 1;
-          for (int pc = 0; pc < np; ++pc) {   // parallel K-split pieces: [pc nk / np, (pc + 1) nk / np)
-            const int k0 = pc * nk / np, k1 = (pc + 1) * nk / np;
-            GemmTile t = mk_tile(i, tm, tn, (tm == 0 && tn == 0 && pc == 0) ? 1 : 0, k1 - k0);
-            if (np > 1) {
-              t.k0 = k0; t.np = np; t.pc = pc;
-              t.part = d.kpart + (size_t)(tm * TN + tn) * np * 4096;
-              t.ctr = pl.d_kctr + (size_t)(nctr + tm * TN + tn);
-            } else {
-              t.ser = d.ksplit;   // serial form (1: no K-split)
-            }
-            pl.tiles.push_back(t);
-          }
-        }
-    if (d.ksplit > 1) nctr += TM * TN;
   }
   if (!pl.f32p && !pl.f32t) {
-    // a launch of more tiles than resident slots (K-split pieces, C4) is dispatched in
-    // order as slots free up: longest first (a no-op without pieces: problems are in ld order)
-    if (pl.tiles.size() > 256 * 3)
-      std::stable_sort(pl.tiles.begin(), pl.tiles.end(), [](const GemmTile& a, const GemmTile& b) { return a.nk > b.nk; });
-    order_tiles_for_cus(pl.tiles, 256, f32_slots());
+    unsigned long long key = 1469598103934665603ull;
+    auto mix = [&](long long v) {
+      for (int b = 0; b < 8; ++b) { key ^= (unsigned long long)((v >> (8 * b)) & 0xFF); key *= 1099511628211ull; }
+    };
+    mix(g_ksplit_par.load()); mix(g_ksplit_bal.load()); mix(g_ksplit_cost.load()); mix(f32_slots());
+    for (int i : order) {
+      const ProbDesc& d = pl.desc[i];
+      mix(i); mix(d.I); mix(d.Ip); mix(d.ld); mix(d.ksplit); mix(wide_prob(d) ? 1 : 0);
+    }
+    if (!tile_cache_get(key, pl.tiles, pl.ksplit_par)) {
+      build_big_tiles(pl, order, wide_prob);
+      tile_cache_put(key, pl.tiles, pl.ksplit_par);
+    }
+    for (GemmTile& t : pl.tiles)   // this call's partial images and counters
+      if (t.np > 1) {
+        const ProbDesc& d = pl.desc[t.prob];
+        const int TN = (d.ld + 63) / 64;
+        t.part = d.kpart + (size_t)(t.tm * TN + t.tn) * t.np * 4096;
+        t.ctr = pl.d_kctr + ctrbase[t.prob] + (size_t)(t.tm * TN + t.tn);
+      }
   }
   std::vector<GemmTile> small;
   for (int i : order) {   // 32 x 64 tiles of the 17..32-row factors
@@ -852,12 +907,16 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   // only the order of the fp64 residual partial sums, never an element's result)
   long long big_elems = 0;
   for (int i : big_jobs) big_elems += (long long)pl.desc[i].I * pl.desc[i].ld;
+  // (also with hist_nv = 1: a lone layer4 factor's 589 k elements made 171 units of three
+  // rows, leaving 85 CUs idle; one-row units spread it over every CU)
   long long hu_big = (long long)kHistElems * pl.hist_nv;
-  if (pl.hist_nv == 2 && g_even_units.load()) {
+  if (g_even_units.load()) {
     const long long slots = 2LL * device_cus();
     int big_maxld = 0;
     for (int i : big_jobs) big_maxld = std::max(big_maxld, pl.desc[i].ld);
-    for (long long t = std::max<long long>(big_maxld, (big_elems + slots - 1) / slots); t < hu_big; t += 256) {
+    // (at least ~1 k elements per unit: below that, the flush atomics outweigh the shorter phases)
+    for (long long t = std::max<long long>({(long long)big_maxld, (big_elems + slots - 1) / slots, 1024LL}); t < hu_big;
+         t += 256) {
       long long units = 0;
       for (int i : big_jobs) {
         const ProbDesc& d = pl.desc[i];
@@ -1479,7 +1538,7 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
       if (diag) { prof_class(ADMMQ_PROF_GEMM); prof_mark(s); } else { prof_pair(ADMMQ_PROF_GEMM, &g0, &g1); }
       if (pl.ntiles_wide + pl.ntiles_small + pl.ntiles_big > 0)
         launch_gemm(pl.d_desc, pl.d_tiles, pl.ntiles_wide, pl.ntiles_small, pl.ntiles_big, pl.split, slot, it, eps,
-                    num_attempts, s, g0, g1);
+                    num_attempts, s, g0, g1, pl.ksplit_par);
       if (pl.nslots > 0)
         launch_gemm_f32p(pl.d_desc, pl.d_tiles + pl.ntiles_wide, pl.d_list_off, pl.nslots, slot, it, eps, num_attempts,
                          s);

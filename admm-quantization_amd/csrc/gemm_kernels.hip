@@ -955,7 +955,8 @@ void launch_split_rows(const ProbDesc* d, int nprob, int maxrows, int which, hip
 int g_gemm_ks_f32 = 1;
 
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,
-                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                 bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                 bool prefetch_u) {
   // tiles[0 .. ntiles_wide) are 256x128 (WM = 8, CW = 2: sixteen waves of 32 x 64, the
   // launches with many rounds of tiles), then ntiles_big 64x64 tiles (WM = 2, four
   // waves, 3-deep ring), then ntiles_small 32x64 tiles (WM = 1: the 17..32-row factors,
@@ -981,6 +982,8 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
       ADMMQ_LAUNCH((k_gemm<2, 2, 3, false>), ntiles_big, 512, t);
     else if (g_gemm_f32_stage == 1) ADMMQ_LAUNCH((k_gemm_f32b<3, true>), ntiles_big, 256, t);
     else if (g_gemm_f32_stage == 2) ADMMQ_LAUNCH((k_gemm_f32b<2, false>), ntiles_big, 256, t);
+    else if (g_gemm_f32_stage == 3 && prefetch_u)   // latency-bound launches (parallel K-split pieces): U before the K-loop
+      ADMMQ_LAUNCH((k_gemm_f32b<3, true>), ntiles_big, 256, t);
     else if (g_gemm_f32_stage == 3) ADMMQ_LAUNCH((k_gemm_f32b<3, false>), ntiles_big, 256, t);
     else if (g_gemm_f32_stage == 4) ADMMQ_LAUNCH((k_gemm_f32b<3, false, true>), ntiles_big, 256, t);
     else ADMMQ_LAUNCH((k_gemm<2, 1, 3, false>), ntiles_big, 256, t);

@@ -452,9 +452,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned s_amax[kTLThreads / 64];
   __shared__ double s_red[kTLThreads / 64][4];
-  __shared__ unsigned long long s_u64[kTLThreads / 64][2];
   __shared__ unsigned long long s_part[kTLBins];
-  __shared__ double s_wmin[kTLThreads / 64];
   __shared__ int s_wcnt[kTLThreads / 64];
   __shared__ int lsel[2 + kMaxSel];
   __shared__ unsigned long long s_best[kTLThreads / 64];
@@ -482,8 +480,6 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   float* const thr = reinterpret_cast<float*>(smem + (size_t)region_a * 4);
   unsigned long long* const h1 = reinterpret_cast<unsigned long long*>(smem + tl_off_h1(region_a, QMAX, n));
   unsigned* const h2 = reinterpret_cast<unsigned*>(smem + tl_off_h2(region_a, QMAX, n));
-  unsigned long long* const H2 = reinterpret_cast<unsigned long long*>(smem + tl_off_H2(region_a, QMAX, n));
-  unsigned long long* const H1 = h1;   // the team totals reuse the block's bins
 
   ThinM m;
   thin_load_m(p, col0, g, m);
@@ -629,44 +625,60 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
       ADMMQ_TL_PH(6);
       if (!team_barrier(&sy.bar, nteam * ++nbar, wait_polls, &s_ok)) { fault = true; break; }
       ADMMQ_TL_PH(7);
-      for (int b = tid; b <= n; b += kTLThreads) { H1[b] = ald_u64(&sy.h1[slot][b]); H2[b] = ald_u64(&sy.h2[slot][b]); }
-      const double S2 = ald_f64(&sy.s2[slot]);
-      __syncthreads();
-      ADMMQ_TL_PH(8);
-      // T(c) = sum_{b > c} H[b]: block suffix sums of H[c + 1] (thread c)
-      const unsigned long long v1 = (tid < n) ? H1[tid + 1] : 0ull, v2 = (tid < n) ? H2[tid + 1] : 0ull;
-      const unsigned long long q1 = wave_suffix_u64(v1), q2 = wave_suffix_u64(v2);
-      if (lane == 0) { s_u64[wave][0] = q1; s_u64[wave][1] = q2; }
-      __syncthreads();
-      unsigned long long T1 = q1, T2 = q2;
+      // ---- the selection by ONE wave (no block barrier inside): lane l owns candidates
+      // 4l .. 4l + 3 (n <= kTLMaxCand = 256) and reads their team totals straight from the
+      // team's bins; T(c) = sum_{b > c} H[b] = the lane's own suffix over its four c plus
+      // the wave suffix of the later lanes' totals; the rigorous bounds of each c, min(A + E)
+      // over the wave, and the ascending list S = {c : A - E <= min} (the same integers and
+      // fp64 operations per candidate as the block form, so the same S)
+      if (wave == 0) {
+        const double S2 = ald_f64(&sy.s2[slot]);
+        unsigned long long a1[4], a2[4];
 #pragma unroll
-      for (int w = 1; w < kTLThreads / 64; ++w)
-        if (w > wave) { T1 += s_u64[w][0]; T2 += s_u64[w][1]; }
-      // the rigorous candidate set S (the same in every workgroup of the team)
-      SelCtx cx;
-      cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * QMAX - 1);
-      cx.u = 0x1p-24;
-      cx.fixu = ldexp(1.0, -K1);
-      cx.Kterm = (double)p.nq * ldexp(1.0, -fixed_exp(mx, p.nq));
-      cx.Nterm = (double)((long long)p.mv.nelem * QMAX);
-      cx.tiny = 8.0 * (double)p.mv.nelem * 0x1p-149;
-      double lo = 1e300, hi = 1e300;
-      if (tid < n) cx.bounds_s((double)s_sc[tid], T1, T2, lo, hi);
-      const double wm = wave_min_f64(hi);
-      if (lane == 0) s_wmin[wave] = wm;
-      __syncthreads();
-      double mn = s_wmin[0];
+        for (int j = 0; j < 4; ++j) {
+          const int c = 4 * lane + j;
+          a1[j] = c < n ? ald_u64(&sy.h1[slot][c + 1]) : 0ull;
+          a2[j] = c < n ? ald_u64(&sy.h2[slot][c + 1]) : 0ull;
+        }
+        ADMMQ_TL_PH(8);
+        unsigned long long l1[4], l2[4], r1 = 0ull, r2 = 0ull;
 #pragma unroll
-      for (int w = 1; w < kTLThreads / 64; ++w) mn = fmin(mn, s_wmin[w]);
-      const bool keep = tid < n && lo <= mn;
-      const unsigned long long bal = __ballot(keep);
-      if (lane == 0) s_wcnt[wave] = __popcll(bal);
-      __syncthreads();
-      int pos = __popcll(bal & ((1ull << lane) - 1ull)), total = 0;
+        for (int j = 3; j >= 0; --j) { r1 += a1[j]; r2 += a2[j]; l1[j] = r1; l2[j] = r2; }
+        const unsigned long long e1 = wave_suffix_u64(r1) - r1, e2 = wave_suffix_u64(r2) - r2;
+        SelCtx cx;
+        cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * QMAX - 1);
+        cx.u = 0x1p-24;
+        cx.fixu = ldexp(1.0, -K1);
+        cx.Kterm = (double)p.nq * ldexp(1.0, -fixed_exp(mx, p.nq));
+        cx.Nterm = (double)((long long)p.mv.nelem * QMAX);
+        cx.tiny = 8.0 * (double)p.mv.nelem * 0x1p-149;
+        double lo[4], hi[4], hmin = 1e300;
 #pragma unroll
-      for (int w = 0; w < kTLThreads / 64; ++w) { pos += w < wave ? s_wcnt[w] : 0; total += s_wcnt[w]; }
-      if (keep && pos < kMaxSel) lsel[2 + pos] = tid;
+        for (int j = 0; j < 4; ++j) {
+          const int c = 4 * lane + j;
+          lo[j] = hi[j] = 1e300;
+          if (c < n) cx.bounds_s((double)s_sc[c], l1[j] + e1, l2[j] + e2, lo[j], hi[j]);
+          hmin = fmin(hmin, hi[j]);
+        }
+        const double mn = wave_min_f64(hmin);
+        unsigned cnt = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cnt += (4 * lane + j < n && lo[j] <= mn) ? 1u : 0u;
+        const unsigned suf = wave_suffix_u32(cnt);   // keeps in lanes >= this one
+        const unsigned tot = __builtin_amdgcn_readfirstlane(suf);   // lane 0: all of them
+        int pos = (int)(tot - suf);                  // keeps in lanes below this one
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = 4 * lane + j;
+          if (c < n && lo[j] <= mn) {
+            if (pos < kMaxSel) lsel[2 + pos] = c;
+            ++pos;
+          }
+        }
+        if (lane == 0) s_wcnt[0] = (int)tot;
+      }
       __syncthreads();
+      const int total = s_wcnt[0];
       const bool all = total > kMaxSel || total == 0;
       const int ns = all ? n : total;
       int cstar;

@@ -109,6 +109,7 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_gemm_stage": (I32, [I32]),
         "admmq_debug_set_ksplit": (I32, [I32]),
         "admmq_debug_set_ksplit_form": (I32, [I32]),
+        "admmq_debug_set_hist_late_hf": (I32, [I32]),
         "admmq_debug_set_ksplit_balance": (I32, [I32, I32]),
         "admmq_debug_ksplit_balance_count": (ctypes.c_int64, [ctypes.c_void_p, I32]),
         "admmq_debug_ksplit_pieces": (I32, [I32, I32]),
@@ -140,6 +141,10 @@ def load() -> ctypes.CDLL:
         "admmq_lowrank_reset": (I32, [P, S, P]),
         "admmq_lowrank_pre": (I32, [P, P, P, P, P, P, I64, F32, P, S, P]),
         "admmq_lowrank_post": (I32, [P, P, P, P, I64, F32, P, S, P]),
+        "admmq_panel_workspace_size": (S, [I64, I64, I64]),
+        "admmq_panel_xtq": (I32, [P, I64, I64, I64, P, I64, P, P, S, P]),
+        "admmq_panel_xy": (I32, [P, I64, I64, I64, P, I64, P, P, S, P]),
+        "admmq_panel_outer": (I32, [P, P, I64, I64, I64, P, I64, P]),
         "admmq_version": (I32, []),
         "admmq_last_error": (ctypes.c_char_p, []),
     }

@@ -27,7 +27,7 @@ from typing import Callable, List, Optional
 
 import torch
 
-from . import _lib
+from . import _lib, panel
 from .quantization import quantize_tensor
 
 
@@ -88,7 +88,9 @@ class KrylovProjector:
     X^T u_i = sigma_i v_i exactly) and the residuals ||X v_i - sigma_i u_i|| / sigma_1; it
     stops when the largest is <= ``tol`` (the truncation then agrees with the exact one to
     about 2 ``tol`` relative: measured on flat spectra, tools/lowrank_bench.py reports it).
-    The products are GEMMs of the tall operand with ``block``-wide panels (hipBLASLt)."""
+    Every pass over X is a hand-written panel kernel (``admmq.panel``: X^T Q, X Y and the
+    final U S V^T, X read as float32 and widened in registers); the re-orthogonalization,
+    the QR of a block and the small eigenproblem are float64 library calls on panels."""
 
     def __init__(self, rank: int, block: int = 32, tol: float = 2e-5, check_every: int = 4, max_blocks: int = 64,
                  seed: int = 0):
@@ -104,10 +106,10 @@ class KrylovProjector:
         # blocks at least `rank` wide: the first Rayleigh-Ritz check then already has r Ritz
         # pairs (a narrower K would index past its eigenpairs and wrap to the top ones)
         k = min(max(self.block, r), m, n)
-        Xd = X.double()
+        Xf = X.float().contiguous()
         if self.Q is None or self.Q.shape != (m, k):
             g = torch.Generator().manual_seed(self.seed)
-            self.Q = torch.linalg.qr(Xd @ torch.randn(n, k, generator=g, dtype=torch.float64).to(X.device))[0]
+            self.Q = torch.linalg.qr(panel.xy(Xf, torch.randn(n, k, generator=g, dtype=torch.float64).to(X.device)))[0]
         blocks = [self.Q]
         K = self.Q
         Q = self.Q
@@ -117,7 +119,7 @@ class KrylovProjector:
             if nb >= self.max_blocks or K.shape[1] + k > min(m, n):
                 do_check = True
             else:
-                Z = Xd @ (Xd.T @ Q)
+                Z = panel.xy(Xf, panel.xtq(Xf, Q))             # X (X^T Q)
                 for _ in range(2):   # full re-orthogonalization against every block so far
                     Z = Z - K @ (K.T @ Z)
                 Q = torch.linalg.qr(Z)[0]
@@ -127,18 +129,21 @@ class KrylovProjector:
                 do_check = nb % self.check_every == 0
             if not do_check:
                 continue
-            B = K.T @ Xd                                   # (nb k) x n
-            evals, evecs = torch.linalg.eigh(B @ B.T)      # ascending
+            Bt = panel.xtq(Xf, K)                              # B^T = X^T K, n x (nb k)
+            evals, evecs = torch.linalg.eigh(Bt.T @ Bt)        # B B^T, ascending
             idx = torch.arange(evals.shape[0] - 1, evals.shape[0] - 1 - k, -1, device=X.device)   # k <= K's columns
             S = torch.sqrt(torch.clamp(evals[idx], min=0.0))
             Ub = evecs[:, idx]
             U = K @ Ub[:, :r]
-            V = (B.T @ Ub[:, :r]) / S[:r]
-            res = float(torch.max(torch.linalg.norm(Xd @ V - U * S[:r], dim=0)) / S[0])
+            V = (Bt @ Ub[:, :r]) / S[:r]
+            res = float(torch.max(torch.linalg.norm(panel.xy(Xf, V) - U * S[:r], dim=0)) / S[0])
             if res <= self.tol or nb >= self.max_blocks or K.shape[1] + k > min(m, n):
                 self.Q = torch.linalg.qr(K @ Ub[:, :k])[0]   # warm start: the leading Ritz vectors
                 self.blocks.append(nb)
                 self.residuals.append(res)
+                if r <= 32:   # the panel kernel's register tile
+                    out = panel.outer((U * S[:r]).contiguous(), V.contiguous())
+                    return out if X.dtype == torch.float32 else out.to(X.dtype)
                 return ((U * S[:r]) @ V.T).to(X.dtype)
 
 

@@ -1,0 +1,84 @@
+"""Panel products of the device rank projection (``scripts/factorize_lowrank.py:80-82``).
+
+``xtq(X, Q) = X^T Q``, ``xy(X, Y) = X Y`` and ``outer(A, B) = A B^T`` over the C-ABI
+(``admmq_panel_*``, ``csrc/panel_kernels.hip``): X is the low-rank loop's float32 iterate,
+read once per product and widened to float64 in registers (v_mfma_f64_16x16x4_f64, fp64
+accumulation in an order fixed by the shapes); the panels are float64. There is no
+fallback: the HIP library must be loaded.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+
+_WS: Dict[torch.device, torch.Tensor] = {}
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    """The partials / arrival counters of the panel kernels, per device, grown on demand and
+    zeroed when (re)allocated (the counters must start at a multiple of the group size)."""
+    ws = _WS.get(dev)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        _WS[dev] = ws
+    return ws
+
+
+def _check_x(X: torch.Tensor) -> torch.Tensor:
+    _lib.require_device(X)
+    if X.dim() != 2 or X.dtype != torch.float32:
+        raise ValueError("admmq.panel: X must be a 2-D float32 device tensor")
+    return X if X.stride(1) == 1 else X.contiguous()
+
+
+def _check_panel(P: torch.Tensor, rows: int, X: torch.Tensor, name: str) -> torch.Tensor:
+    if P.dim() != 2 or P.shape[0] != rows or P.dtype != torch.float64 or P.device != X.device:
+        raise ValueError(f"admmq.panel: {name} must be a float64 tensor with {rows} rows on X's device")
+    return P.contiguous()
+
+
+def xtq(X: torch.Tensor, Q: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``X^T Q`` (n x k float64) for X m x n float32, Q m x k float64."""
+    X = _check_x(X)
+    m, n = X.shape
+    Q = _check_panel(Q, m, X, "Q")
+    k = Q.shape[1]
+    Y = out if out is not None else torch.empty(n, k, dtype=torch.float64, device=X.device)
+    lib = _lib.load()
+    nb = lib.admmq_panel_workspace_size(m, n, k)
+    ws = _workspace(X.device, nb)
+    _lib.check(lib.admmq_panel_xtq(_lib.ptr(X), m, n, X.stride(0), _lib.ptr(Q), k, _lib.ptr(Y), _lib.ptr(ws),
+                                   ws.numel(), _lib.stream_handle(X.device)), "panel_xtq")
+    return Y
+
+
+def xy(X: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``X Y`` (m x k float64) for X m x n float32, Y n x k float64."""
+    X = _check_x(X)
+    m, n = X.shape
+    Y = _check_panel(Y, n, X, "Y")
+    k = Y.shape[1]
+    Z = out if out is not None else torch.empty(m, k, dtype=torch.float64, device=X.device)
+    lib = _lib.load()
+    nb = lib.admmq_panel_workspace_size(m, n, k)
+    ws = _workspace(X.device, nb)
+    _lib.check(lib.admmq_panel_xy(_lib.ptr(X), m, n, X.stride(0), _lib.ptr(Y), k, _lib.ptr(Z), _lib.ptr(ws),
+                                  ws.numel(), _lib.stream_handle(X.device)), "panel_xy")
+    return Z
+
+
+def outer(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``A B^T`` rounded once to float32 (m x n) for A m x r, B n x r float64, r <= 32."""
+    _lib.require_device(A)
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[1] or A.dtype != torch.float64 or B.dtype != torch.float64:
+        raise ValueError("admmq.panel.outer: A (m x r) and B (n x r) float64 with one r")
+    A, B = A.contiguous(), B.contiguous()
+    m, r = A.shape
+    n = B.shape[0]
+    O = out if out is not None else torch.empty(m, n, dtype=torch.float32, device=A.device)
+    _lib.check(_lib.load().admmq_panel_outer(_lib.ptr(A), _lib.ptr(B), m, n, r, _lib.ptr(O), O.stride(0),
+                                             _lib.stream_handle(A.device)), "panel_outer")
+    return O

@@ -96,11 +96,13 @@ struct ProbDesc {
 struct QJob {
   const float* src;   // rows x cols contiguous (user)
   float* dst;         // rows x cols contiguous (user)
-  float* Xp;          // padded copy rows x ld (workspace)
+  float* Xp;          // padded copy rows x ld (workspace), or src itself when cols % 4 == 0
   MseView mv;         // one slot
   int rows, cols, ld, nq;
   float tmin_kw, tmax_kw;   // affine kwargs (NaN = unset)
-  int has_kw, pad_;
+  int has_kw, copy;         // copy: Xp is the workspace copy (k_qpack writes it)
+  unsigned* pstat;          // k_qpack's per-unit {absmax, min, max} partials (3 per unit)
+  int pu0, pun;             // this job's units in the statistics launch: first, count
 };
 
 // Work-unit tables (built on the host, uploaded once per call)
@@ -223,6 +225,7 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
                  hipEvent_t ev1 = nullptr, bool prefetch_u = false);
 extern int g_gemm_ks_f32;
 extern int g_gemm_f32_stage;   // fp32 64 x 64 staging form (gemm_kernels.hip)
+extern int g_hist_late_hf;     // fused search: finalize loads after the wait (mse_search.hip)
 void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
                       hipStream_t s);
 void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,
@@ -265,7 +268,7 @@ void launch_finalize_admm(const ProbDesc* d, const Chunk* chunks, int nchunks, i
                           int qscheme, int slot, int iter, hipStream_t s);
 void launch_unpack(const ProbDesc* d, int nprob, int maxI, int maxR, hipStream_t s);
 
-void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s);
+void launch_qpack(const QJob* jobs, int njobs, const Chunk* chunks, int nchunks, hipStream_t s);
 void launch_channel_quant(const float* x, float* y, long long A, int C, long long B, long long outer, int L, int Lo,
                           unsigned* stats, int bits, int scheme, hipStream_t s);
 void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
@@ -277,6 +280,7 @@ constexpr int kHistMultiRounds = 2;   // non-fused search: units per block sized
 constexpr int kHistMultiMaxReps = 8;  // ... at most 8 units per block
 constexpr int kHistMaxUnits = 512;  // stage-1 units that fit in one round (2 per CU): above, 2x larger units
 constexpr int kElemChunk = 1024;    // elements per elementwise work unit (256 threads x float4)
+constexpr int kPackElems = 16384;   // elements per k_qpack unit (256 threads x 16 float4): few partials
 constexpr int kFinElems = 4096;     // elements per ADMM finalize work unit when there are >= kFinMinUnits of them
 constexpr int kFinMinUnits = 256;   //   (else kElemChunk: small problem sets keep their parallelism)
 

@@ -423,7 +423,6 @@ struct AdmmPlan {
   std::vector<Chunk> sse_chunks, fin_chunks, hist_chunks;
   std::vector<Chunk> hist_multi;   // the same units, several per block (launches without the fused finalize)
   Chunk* d_hist_multi = nullptr;
-  Chunk* d_hist_fin = nullptr;     // fused finalize with several units per block (built in run)
   int nhm_big = 0;                 // hist_multi blocks of the big jobs (listed first)
   ProbDesc* d_desc = nullptr;
   GemmTile* d_tiles = nullptr;
@@ -907,16 +906,15 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   // only the order of the fp64 residual partial sums, never an element's result)
   long long big_elems = 0;
   for (int i : big_jobs) big_elems += (long long)pl.desc[i].I * pl.desc[i].ld;
-  // (also with hist_nv = 1: a lone layer4 factor's 589 k elements made 171 units of three
-  // rows, leaving 85 CUs idle; one-row units spread it over every CU)
+  // (not with hist_nv = 1: a lone layer4 factor's 589 k elements in 512 one-row units
+  // instead of 171 three-row ones made its search 22 -> 27 us - the flush atomics and the
+  // ticket chain grow with the block count faster than the per-block phases shrink)
   long long hu_big = (long long)kHistElems * pl.hist_nv;
-  if (g_even_units.load()) {
+  if (pl.hist_nv == 2 && g_even_units.load()) {
     const long long slots = 2LL * device_cus();
     int big_maxld = 0;
     for (int i : big_jobs) big_maxld = std::max(big_maxld, pl.desc[i].ld);
-    // (at least ~1 k elements per unit: below that, the flush atomics outweigh the shorter phases)
-    for (long long t = std::max<long long>({(long long)big_maxld, (big_elems + slots - 1) / slots, 1024LL}); t < hu_big;
-         t += 256) {
+    for (long long t = std::max<long long>(big_maxld, (big_elems + slots - 1) / slots); t < hu_big; t += 256) {
       long long units = 0;
       for (int i : big_jobs) {
         const ProbDesc& d = pl.desc[i];
@@ -996,7 +994,6 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   pl.d_fin = cv.take<Chunk>(pl.fin_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_hist_multi = cv.take<Chunk>(pl.hist_multi.size());
-  pl.d_hist_fin = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_small = cv.take<int>(std::max<size_t>(pl.small.size(), 1));
   pl.d_thin = cv.take<ThinLoopUnit>(pl.thin.size());
   if ((int)pl.small.size() == nprob) {   // sized by the problems alone (not by the device's CUs)
@@ -1068,9 +1065,10 @@ __global__ void k_export_info(const ProbDesc* __restrict__ d, int n, int32_t* in
 // Standalone quantization
 struct QPlan {
   std::vector<QJob> jobs;
-  std::vector<Chunk> pack_chunks, sse_chunks, hist_chunks;
+  std::vector<Chunk> pack_chunks, stat_chunks, sse_chunks, hist_chunks;
   QJob* d_jobs = nullptr;
   Chunk* d_pack = nullptr;
+  Chunk* d_stat = nullptr;
   Chunk* d_sse = nullptr;
   Chunk* d_hist = nullptr;
   unsigned short* d_rank0 = nullptr;    // merged stage-1 order (kMaxMerged), then the cell index (kCells + 2)
@@ -1093,24 +1091,32 @@ static int plan_quant(const admmq_qtensor* t, int n, int ncand, void* ws, QPlan&
     if ((long long)j.rows * j.ld >= (1LL << 31)) return fail(ADMMQ_ERR_ARG, "tensor too large");
     j.nq = j.rows * (j.ld / 4);
     j.has_kw = t[i].has_minmax; j.tmin_kw = t[i].tmin; j.tmax_kw = t[i].tmax;
-    j.Xp = cv.take<float>((size_t)j.rows * j.ld);
+    j.Xp = cv.take<float>((size_t)j.rows * j.ld);   // (carved either way: the size does not depend on src)
+    j.copy = !(j.cols % 4 == 0 && (reinterpret_cast<uintptr_t>(j.src) & 15) == 0);
+    if (!j.copy) j.Xp = const_cast<float*>(j.src);   // read in place (only k_qpack's copy writes Xp)
     carve_view(cv, j.mv, 1, ncand);
     j.mv.X = j.Xp; j.mv.rows = j.rows; j.mv.cols = j.cols; j.mv.ld = j.ld; j.mv.qpr = j.ld / 4;
     j.mv.nq = j.nq; j.mv.nelem = j.rows * j.cols; j.mv.done = nullptr;
   }
   pl.pack_chunks.clear();
+  pl.stat_chunks.clear();
   pl.sse_chunks.clear();
   pl.hist_chunks.clear();
   for (int i = 0; i < n; ++i) {
     const QJob& j = pl.jobs[i];
     const long long tot = (long long)j.rows * j.ld;
     for (long long e = 0; e < tot; e += kElemChunk) pl.pack_chunks.push_back({i, (int)e});
+    pl.jobs[i].pu0 = (int)pl.stat_chunks.size();
+    for (long long e = 0; e < tot; e += kPackElems) pl.stat_chunks.push_back({i, (int)e});
+    pl.jobs[i].pun = (int)pl.stat_chunks.size() - pl.jobs[i].pu0;
     for (int q = 0; q < j.nq; q += kSseQuads) pl.sse_chunks.push_back({i, q});
     for (long long e = 0; e < tot; e += kHistElems) pl.hist_chunks.push_back({i, (int)e, j.mv.stat, nullptr, j.Xp, nullptr, tot});
     pl.jobs[i].mv.nhist = (int)((tot + kHistElems - 1) / kHistElems);
   }
   pl.d_jobs = cv.take<QJob>(n);
   pl.d_pack = cv.take<Chunk>(pl.pack_chunks.size());
+  pl.d_stat = cv.take<Chunk>(pl.stat_chunks.size());
+  for (int i = 0; i < n; ++i) pl.jobs[i].pstat = cv.take<unsigned>(3 * (size_t)pl.jobs[i].pun);
   pl.d_sse = cv.take<Chunk>(pl.sse_chunks.size());
   pl.d_hist = cv.take<Chunk>(pl.hist_chunks.size());
   pl.d_rank0 = cv.take<unsigned short>(kMaxMerged + kCells + 2);
@@ -1140,10 +1146,11 @@ static int run_quant(QPlan& pl, int n, int bits, int qscheme, int ncand, hipStre
   int rc;
   if ((rc = h2d(pl.d_jobs, pl.jobs.data(), n * sizeof(QJob), s))) return rc;
   if ((rc = h2d(pl.d_pack, pl.pack_chunks.data(), pl.pack_chunks.size() * sizeof(Chunk), s))) return rc;
+  if ((rc = h2d(pl.d_stat, pl.stat_chunks.data(), pl.stat_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_sse, pl.sse_chunks.data(), pl.sse_chunks.size() * sizeof(Chunk), s))) return rc;
   if ((rc = h2d(pl.d_hist, pl.hist_chunks.data(), pl.hist_chunks.size() * sizeof(Chunk), s))) return rc;
   hipLaunchKernelGGL(k_qinit, dim3(n), dim3(256), 0, s, pl.d_jobs, n, ncand);
-  launch_qpack(pl.d_jobs, pl.d_pack, (int)pl.pack_chunks.size(), s);
+  launch_qpack(pl.d_jobs, n, pl.d_stat, (int)pl.stat_chunks.size(), s);
   if (qscheme == kMse) {
     const bool all = exhaustive || !two_stage_ok(ncand, bits);
     std::vector<unsigned short> rank0, groups;
@@ -1308,6 +1315,13 @@ int64_t admmq_debug_ksplit_balance_count(const int32_t* IR, int32_t nprob) {
     }
   }
   return ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
+}
+// diagnostics: the fused search's finalize loads (H, F) issued after the wait for the job's
+// selection (1) instead of before it (0, default); same results
+int32_t admmq_debug_set_hist_late_hf(int32_t on) {
+  if (on < 0 || on > 1) return fail(ADMMQ_ERR_ARG, "late_hf must be 0 or 1");
+  g_hist_late_hf = on;
+  return ADMMQ_OK;
 }
 // diagnostics: the K-split pieces the planner gives an (I, R) factor (0 on bad arguments)
 int32_t admmq_debug_ksplit_pieces(int32_t I, int32_t R) {
@@ -1479,38 +1493,12 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   const int fin_cap = fin_ok ? (cap_over > 0 ? std::min(cap_over, hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
                                              : hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
                              : 0;
-  // more units than resident blocks: each block takes `fin_reps` consecutive units of its job
-  // (one table setup, flush and wait for all of them; their finalize re-reads the elements)
-  int fin_reps = 1, nfin_blocks = nh_big;
-  std::vector<Chunk> fin_multi;
-  // (measured at C4: no faster than the separate finalize launch, 324 vs 318 ms per sweep -
-  // the per-block serialization of reps units outweighs the saved launch; so only when a
-  // diagnostic budget asks for it)
-  if (fin_ok && fin_cap > 0 && nh_big > fin_cap && cap_over > 0) {
-    for (fin_reps = 2; fin_reps <= kHistMultiMaxReps; ++fin_reps) {
-      fin_multi.clear();
-      for (int a = 0; a < nh_big;) {
-        int b = a;
-        while (b < nh_big && pl.hist_chunks[b].job == pl.hist_chunks[a].job) ++b;
-        const int nblk = (b - a + fin_reps - 1) / fin_reps;
-        for (int c = a; c < b; c += fin_reps) {
-          const int e = std::min(b, c + fin_reps) - 1;
-          Chunk k = pl.hist_chunks[c];
-          k.reps = e - c + 1;
-          k.step = (int)(pl.hist_chunks[c].total - pl.hist_chunks[c].start);
-          k.total = pl.hist_chunks[e].total;
-          k.nblk = nblk;
-          fin_multi.push_back(k);
-        }
-        a = b;
-      }
-      if ((int)fin_multi.size() <= fin_cap) break;
-    }
-    nfin_blocks = (int)fin_multi.size();
-  }
+  // one whole-row unit per block, all blocks resident; a launch with more units than that
+  // takes the separate finalize launch (round 3 measured blocks taking several units each
+  // with the finalize fused: no faster at C4, 324 vs 318 ms per sweep, and that path held
+  // the fused kernel at 40 spilled VGPRs)
+  const int nfin_blocks = nh_big;
   const bool fuse_fin = fin_ok && fin_cap > 0 && nfin_blocks <= fin_cap;
-  if (fuse_fin && fin_reps > 1 && (rc = h2d(pl.d_hist_fin, fin_multi.data(), fin_multi.size() * sizeof(Chunk), s)))
-    return rc;
   const unsigned polls = g_fin_wait_polls.load();
   if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned), s) != hipSuccess)
     return check_hip("ready reset");
@@ -1555,13 +1543,13 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
     if (qscheme == kMse) {
       // two-stage: stage 1, the selection and (when |S| > 1) stage 2 all in the hist launch
       if (!exhaustive && merged) {
-        // fused finalize: one whole-row unit per block; otherwise several units per block
+        // fused finalize: one whole-row unit per block; otherwise possibly several units per block
         const int nh = fuse_fin ? nfin_blocks : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
         if (nh > 0) {
           hipEvent_t h0, h1;
           prof_pair(ADMMQ_PROF_SEARCH, &h0, &h1);
           launch_mse_hist3(pl.d_desc, nullptr,
-                           fuse_fin ? (fin_reps > 1 ? pl.d_hist_fin : pl.d_hist) : pl.d_hist_multi, nh, num_attempts,
+                           fuse_fin ? pl.d_hist : pl.d_hist_multi, nh, num_attempts,
                            bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s, h0, h1);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each

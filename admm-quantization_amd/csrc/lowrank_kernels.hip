@@ -6,13 +6,15 @@
 //     U += H - H_ ;  r = |H - H_|^2/|H|^2 ;  s = |H - H_prev|^2/|U|^2 ;  break if r, s < eps
 //                                                       k_lr_post  (H_prev is the old H)
 //
-// Both kernels are elementwise streams (HBM-bound: pre 20 B/element, post 20 B/element
-// + the projection's own pass); every float32 operation is in the reference's order.
+// Both kernels are elementwise streams (HBM-bound: pre 24 B/element, post 20 B/element
+// + the projection's own pass; float4 when aligned); every float32 operation is in the reference's order.
 // The break test runs on the device: post's blocks write fp64 partial sums, the last
 // block to arrive sums them in block order (deterministic), tests r < eps and s < eps
 // and sets the sticky `done` word; later pre/post launches see it and do nothing, so
 // the caller queues all max_iter-1 iterations without a host round trip per iteration.
 #include <algorithm>
+#include <cstdint>
+#include <initializer_list>
 #include <string>
 
 #include "../../include/admmq.h"
@@ -27,16 +29,35 @@ struct LrState {
   int done, ticket, iters, pad_;
 };
 
+// V4: every pointer 16-byte aligned and n % 4 == 0 (the host checks): float4 streams
+template <bool V4>
 __global__ __launch_bounds__(kLrThreads) void k_lr_pre(const float* __restrict__ H, const float* __restrict__ U,
                                                        const float* __restrict__ W, const float* __restrict__ H2,
                                                        float* __restrict__ Hbar, float* __restrict__ X, long long n,
                                                        float rho, float den, const LrState* __restrict__ st) {
   if (st->done) return;
-  for (long long e = (long long)blockIdx.x * kLrThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kLrThreads) {
-    const float hu = H[e] + U[e];
-    const float t = ((rho * hu + W[e]) - H2[e]) / den;   // (rho*(H + U) + W - H2) / (1 + rho)
-    Hbar[e] = t;
-    X[e] = t - U[e];
+  auto one = [&](float h, float u, float w, float h2, float& hb, float& x) {
+    const float hu = h + u;
+    const float t = ((rho * hu + w) - h2) / den;   // (rho*(H + U) + W - H2) / (1 + rho)
+    hb = t;
+    x = t - u;
+  };
+  if constexpr (V4) {
+    const long long n4 = n >> 2;
+    for (long long q = (long long)blockIdx.x * kLrThreads + threadIdx.x; q < n4; q += (long long)gridDim.x * kLrThreads) {
+      const float4 h = reinterpret_cast<const float4*>(H)[q], u = reinterpret_cast<const float4*>(U)[q];
+      const float4 w = reinterpret_cast<const float4*>(W)[q], h2 = reinterpret_cast<const float4*>(H2)[q];
+      float4 hb, x;
+      one(h.x, u.x, w.x, h2.x, hb.x, x.x);
+      one(h.y, u.y, w.y, h2.y, hb.y, x.y);
+      one(h.z, u.z, w.z, h2.z, hb.z, x.z);
+      one(h.w, u.w, w.w, h2.w, hb.w, x.w);
+      reinterpret_cast<float4*>(Hbar)[q] = hb;
+      reinterpret_cast<float4*>(X)[q] = x;
+    }
+  } else {
+    for (long long e = (long long)blockIdx.x * kLrThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kLrThreads)
+      one(H[e], U[e], W[e], H2[e], Hbar[e], X[e]);
   }
 }
 
@@ -46,25 +67,47 @@ __device__ __forceinline__ double lr_wave_sum(double v) {
   return v;
 }
 
+template <bool V4>
 __global__ __launch_bounds__(kLrThreads) void k_lr_post(const float* __restrict__ Hn, const float* __restrict__ Hbar,
                                                         float* __restrict__ H, float* __restrict__ U, long long n,
                                                         float eps, LrState* __restrict__ st, double* __restrict__ part) {
   if (st->done) return;
-  // contiguous chunk per block: the block partials do not depend on the grid schedule
-  const long long per = (n + gridDim.x - 1) / gridDim.x;
-  const long long b0 = (long long)blockIdx.x * per, b1 = min(n, b0 + per);
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
-  for (long long e = b0 + threadIdx.x; e < b1; e += kLrThreads) {
-    const float hn = Hn[e], hb = Hbar[e], hp = H[e];
+  auto one = [&](float hn, float hb, float hp, float& u) {
     const float d = hn - hb;
-    const float u = U[e] + d;                    // U += H - H_
-    U[e] = u;
-    H[e] = hn;
+    u = u + d;                                   // U += H - H_
     const float dp = hn - hp;
     s1 += (double)d * d;                         // sum (H - H_)^2
     s2 += (double)hn * hn;                       // sum H^2
     s3 += (double)dp * dp;                       // sum (H - H_prev)^2
     s4 += (double)u * u;                         // sum U^2
+  };
+  // contiguous chunk per block: the block partials do not depend on the grid schedule
+  if constexpr (V4) {
+    const long long n4 = n >> 2;
+    const long long per = (n4 + gridDim.x - 1) / gridDim.x;
+    const long long b0 = (long long)blockIdx.x * per, b1 = min(n4, b0 + per);
+    for (long long q = b0 + threadIdx.x; q < b1; q += kLrThreads) {
+      const float4 hn = reinterpret_cast<const float4*>(Hn)[q], hb = reinterpret_cast<const float4*>(Hbar)[q];
+      const float4 hp = reinterpret_cast<const float4*>(H)[q];
+      float4 u = reinterpret_cast<const float4*>(U)[q];
+      one(hn.x, hb.x, hp.x, u.x);
+      one(hn.y, hb.y, hp.y, u.y);
+      one(hn.z, hb.z, hp.z, u.z);
+      one(hn.w, hb.w, hp.w, u.w);
+      reinterpret_cast<float4*>(U)[q] = u;
+      reinterpret_cast<float4*>(H)[q] = hn;
+    }
+  } else {
+    const long long per = (n + gridDim.x - 1) / gridDim.x;
+    const long long b0 = (long long)blockIdx.x * per, b1 = min(n, b0 + per);
+    for (long long e = b0 + threadIdx.x; e < b1; e += kLrThreads) {
+      const float hn = Hn[e], hb = Hbar[e], hp = H[e];
+      float u = U[e];
+      one(hn, hb, hp, u);
+      U[e] = u;
+      H[e] = hn;
+    }
   }
   __shared__ double red[4][kLrThreads / 64];
   __shared__ int last;
@@ -95,6 +138,13 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_post(const float* __restrict_
 
 static size_t lr_bytes() { return 256 + (size_t)kLrBlocks * 4 * sizeof(double); }
 
+static bool aligned16(std::initializer_list<const float*> ps) {
+  for (const float* p : ps)
+    if (reinterpret_cast<uintptr_t>(p) & 15) return false;
+  return true;
+}
+
+// units = elements (scalar) or float4s (V4)
 static int lr_grid(long long n) { return (int)std::max(1LL, std::min<long long>(kLrBlocks, (n + kLrThreads - 1) / kLrThreads)); }
 
 }  // namespace admmq
@@ -118,8 +168,14 @@ int32_t admmq_lowrank_pre(const float* H, const float* U, const float* W, const 
   if (!workspace || workspace_bytes < lr_bytes()) return set_error(ADMMQ_ERR_WORKSPACE, "lowrank: workspace too small");
   if (n == 0) return ADMMQ_OK;
   const LrState* st = static_cast<const LrState*>(workspace);
-  hipLaunchKernelGGL(k_lr_pre, dim3(lr_grid(n)), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), H, U, W, H2,
-                     Hbar, X, (long long)n, rho, 1.0f + rho, st);
+  const bool v4 = n % 4 == 0 && aligned16({H, U, W, H2, Hbar, X});
+  const int grid = lr_grid(v4 ? n / 4 : n);
+  if (v4)
+    hipLaunchKernelGGL(k_lr_pre<true>, dim3(grid), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), H, U, W, H2,
+                       Hbar, X, (long long)n, rho, 1.0f + rho, st);
+  else
+    hipLaunchKernelGGL(k_lr_pre<false>, dim3(grid), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), H, U, W, H2,
+                       Hbar, X, (long long)n, rho, 1.0f + rho, st);
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "lowrank_pre: launch failed");
 }
 
@@ -129,8 +185,14 @@ int32_t admmq_lowrank_post(const float* Hn, const float* Hbar, float* H, float* 
   if (!workspace || workspace_bytes < lr_bytes()) return set_error(ADMMQ_ERR_WORKSPACE, "lowrank: workspace too small");
   LrState* st = static_cast<LrState*>(workspace);
   double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256);
-  hipLaunchKernelGGL(k_lr_post, dim3(lr_grid(n)), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), Hn, Hbar, H,
-                     U, (long long)n, eps, st, part);
+  const bool v4 = n % 4 == 0 && aligned16({Hn, Hbar, H, U});
+  const int grid = lr_grid(v4 ? n / 4 : n);
+  if (v4)
+    hipLaunchKernelGGL(k_lr_post<true>, dim3(grid), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), Hn, Hbar, H,
+                       U, (long long)n, eps, st, part);
+  else
+    hipLaunchKernelGGL(k_lr_post<false>, dim3(grid), dim3(kLrThreads), 0, static_cast<hipStream_t>(stream), Hn, Hbar, H,
+                       U, (long long)n, eps, st, part);
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "lowrank_post: launch failed");
 }
 

@@ -505,6 +505,71 @@ __device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned lon
 }
 
 
+// The same selection by ONE wave for n <= 256 (the last stage-1 block of a job): lane l owns
+// candidates 4l .. 4l + 3, sums their kHistRep replicas straight from the job's global
+// histograms (sc1 atomic loads), computes their bounds (the same fp64 operations per
+// candidate as select_block, so the same S), the wave min of A + E and the ascending list
+// by a wave prefix count - no block barrier until the final one (lsel visible to every
+// thread). Called by every thread of the block.
+__device__ void select_wave4(const MseView& v, int* sel, int* lsel, const unsigned long long* G1,
+                             const unsigned long long* G2, int slot, float mx, int n, int qmax) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned long long t1[4], t2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { t1[j] = 0ull; t2[j] = 0ull; }
+#pragma unroll
+    for (int r = 0; r < kHistRep; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * lane + j;
+        if (c < n) {
+          t1[j] += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t2[j] += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    SelCtx cx;
+    cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * qmax - 1);
+    cx.u = 0x1p-24;
+    cx.fixu = ldexp(1.0, -hist_fixed_exp(mx, v.nelem, qmax));
+    cx.Kterm = (double)v.nq * ldexp(1.0, -fixed_exp(mx, v.nq));
+    cx.Nterm = (double)((long long)v.nelem * qmax);
+    cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
+    double lo[4], hi[4], hmin = 1e300;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * lane + j;
+      lo[j] = hi[j] = 1e300;
+      if (c < n) cx.bounds(c, t1[j], t2[j], lo[j], hi[j]);
+      hmin = fmin(hmin, hi[j]);
+    }
+    const double mn = wave_min_f64(hmin);
+    unsigned cnt = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cnt += (4 * lane + j < n && lo[j] <= mn) ? 1u : 0u;
+    const unsigned suf = wave_suffix_u32(cnt);                   // keeps in lanes >= this one
+    const int total = (int)__builtin_amdgcn_readfirstlane(suf);   // lane 0: all of them
+    int pos = total - (int)suf;                                    // keeps in lanes below
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * lane + j;
+      if (c < n && lo[j] <= mn) {
+        if (pos < kMaxSel) { sel[2 + pos] = c; lsel[2 + pos] = c; }
+        ++pos;
+      }
+    }
+    if (lane == 0) {
+      if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
+      else { sel[0] = total; sel[1] = 0; }
+      lsel[0] = sel[0]; lsel[1] = sel[1];
+      if (ADMMQ_TRACE) atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
+    }
+  }
+  __syncthreads();
+}
+
 // Rank-by-counting of the thresholds (fallback when the host order does not hold):
 // rows thr[j][.] are non-decreasing; with the order (value, level, candidate)
 // rank(k, c) = sum_{j<k} #{row j <= T} + c + sum_{j>k} #{row j < T}, L = sum_j #{row j <= T}.
@@ -873,7 +938,14 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
 // with a stale selection record; the caller re-runs the call with the separate finalize
 // launch (the PyTorch op does). Saves the finalize launch, its dependent parameter chain
 // and its re-read of H_T and U.
-template <int QMAX, int NV, bool FIN>
+// LATE (FIN only): the finalize's H / F loads are issued after the wait for the job's
+// selection instead of before it (fewer registers live across the wait, one more load
+// latency on the finalize path)
+#ifndef ADMMQ_FIN_STREAM
+#define ADMMQ_FIN_STREAM 1
+#endif
+constexpr bool kFinStream = ADMMQ_FIN_STREAM != 0;   // the fused finalize stores each group at once
+template <int QMAX, int NV, bool FIN, bool LATE = false>
 __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     const ProbDesc* __restrict__ d, const QJob* __restrict__ qj, const Chunk* __restrict__ chunks, int ncand, int slot,
     const unsigned short* __restrict__ rank0, const unsigned short* __restrict__ groups, int ngroups, int bits,
@@ -925,32 +997,18 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   };
   if (mse_degenerate(mx)) {     // the projection emits NaN for degenerate mx (no search)
     if (ck.start == 0 && threadIdx.x == 0) { sel[0] = 1; sel[1] = 0; }
-    if constexpr (FIN) {
+    if constexpr (FIN) {   // (one unit per block)
       const ProbDesc& p = d[ck.job];
-      const int nu = max(ck.reps, 1);
-      for (int r = 0; r < nu; ++r) {   // every unit of the block (several: re-read its elements)
-        const long long ub = (long long)ck.start + (long long)r * ck.step;
-        const long long ue = nu > 1 ? min(ub + ck.step, total) : total;
-        if (nu > 1) {
 #pragma unroll
-          for (int hh = 0; hh < 2 * NV; ++hh) {
-            const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-            const long long ec = e < ue ? e : 0;
-            x4[hh] = gld4(ck.X + ec);
-            u4[hh] = gld4(ck.U + ec);
-          }
-        }
-#pragma unroll
-        for (int hh = 0; hh < 2 * NV; ++hh) {
-          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-          const long long ec = e < ue ? e : 0;
-          h4[hh] = gld4(ck.H + ec);
-          f4[hh] = gld4(ck.F + ec);
-        }
-        if (r > 0) __syncthreads();
-        admm_finalize_block<kH3Threads, 2 * NV>(p, ub, ue, x4, u4, h4, f4, qparams_mse(bits, __builtin_nanf("")), slot,
-                                                iter, blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
+      for (int hh = 0; hh < 2 * NV; ++hh) {
+        const long long e = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+        const long long ec = e < total ? e : 0;
+        h4[hh] = gld4(ck.H + ec);
+        f4[hh] = gld4(ck.F + ec);
       }
+      admm_finalize_block<kH3Threads, 2 * NV, kFinStream>(p, ck.start, total, x4, u4, h4, f4,
+                                                    qparams_mse(bits, __builtin_nanf("")), slot, iter,
+                                                    blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem));
     }
     return;
   }
@@ -971,9 +1029,9 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   const int dummy = M + 1 + (threadIdx.x & 63);
   double s2 = 0.0;
   // a block may take several consecutive units of its job (ck.reps, `step` elements each):
-  // one table setup and one flush for all of them (FIN: only when the launch has more
-  // units than resident blocks; the finalize then re-reads each unit's elements)
-  const int reps = max(ck.reps, 1);
+  // one table setup and one flush for all of them (not FIN: the fused finalize's launch
+  // has one unit per block, all resident)
+  const int reps = FIN ? 1 : max(ck.reps, 1);
   for (int r = 0; r < reps; ++r) {
     const long long ub = (long long)ck.start + (long long)r * ck.step;   // unit r (r > 0: reps > 1 only)
     const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
@@ -1042,7 +1100,9 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
     const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
-    if (n <= (int)blockDim.x) {
+    if (n <= 256) {
+      select_wave4(v, sel, lsel, G1, G2, slot, mx, n, QMAX);
+    } else if (n <= (int)blockDim.x) {
       const int c = threadIdx.x;
       unsigned long long t1 = 0ull, t2 = 0ull;
       if (c < n) {
@@ -1091,7 +1151,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   }
   if constexpr (FIN) {
     const ProbDesc& p = d[ck.job];
-    if (reps == 1) load_hf();   // (several units: re-read per unit below)
+    if (!LATE) load_hf();
     if (!last) {   // wait for the job's selection (bounded)
       if (threadIdx.x == 0) {
         unsigned polls = 0;
@@ -1114,6 +1174,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
         return;
       }
     }
+    if (LATE) load_hf();
     QParams qp;
     if (lsel[0] == 1) {
       qp = qparams_mse(bits, cand_t(mx, lsel[2], n));
@@ -1127,28 +1188,9 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     }
     __syncthreads();   // the search tables' LDS is reused as rmax
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) g_hist_trace[blockIdx.x][5] = ADMMQ_NOW();
-    if (reps == 1) {
-      admm_finalize_block<kH3Threads, 2 * NV>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
-                                              blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem),
-                                              ADMMQ_TRACE && blockIdx.x < kHistTraceMax ? g_fin_trace[blockIdx.x] : nullptr);
-    } else {
-      for (int r = 0; r < reps; ++r) {   // each unit's H_T, U, H, F again (L2-resident), then its finalize step
-        const long long ub = (long long)ck.start + (long long)r * ck.step;
-        const long long ue = min(ub + ck.step, total);
-#pragma unroll
-        for (int hh = 0; hh < 2 * NV; ++hh) {
-          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-          const long long ec = e < ue ? e : 0;
-          x4[hh] = gld4(ck.X + ec);
-          u4[hh] = gld4(ck.U + ec);
-          h4[hh] = gld4(ck.H + ec);
-          f4[hh] = gld4(ck.F + ec);
-        }
-        __syncthreads();   // rmax / the reduction scratch of the previous unit are free again
-        admm_finalize_block<kH3Threads, 2 * NV>(p, ub, ue, x4, u4, h4, f4, qp, slot, iter, blockIdx.x & (kResRep - 1),
-                                                reinterpret_cast<unsigned*>(smem), nullptr);
-      }
-    }
+    admm_finalize_block<kH3Threads, 2 * NV, kFinStream>(p, ck.start, total, x4, u4, h4, f4, qp, slot, iter,
+                                                  blockIdx.x & (kResRep - 1), reinterpret_cast<unsigned*>(smem),
+                                                  ADMMQ_TRACE && blockIdx.x < kHistTraceMax ? g_fin_trace[blockIdx.x] : nullptr);
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
       // columns 4, 5: {wait for the selection done, finalize done} (the search ended at 3 / 4)
       const unsigned long long tw = g_hist_trace[blockIdx.x][5];
@@ -1398,6 +1440,7 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
 bool merged_ok(int ncand, int bits) {
   return ncand >= 2 && ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist3_lds_bytes(ncand, bits) <= 150 * 1024;
 }
+int g_hist_late_hf = 0;   // fused search: the finalize's H / F loads after the wait (k_mse_hist3 LATE)
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
                       unsigned wait_polls, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -1407,9 +1450,13 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
 #define ADMMQ_H3(Q, V, F)                                                                                         \
   hipExtLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, chunks, \
                         ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
+#define ADMMQ_H3L(Q)                                                                                               \
+  hipExtLaunchKernelGGL((k_mse_hist3<Q, 2, true, true>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, \
+                        chunks, ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
 #define ADMMQ_H3N(Q)                               \
   if (fin) {                                       \
-    if (nv == 2) ADMMQ_H3(Q, 2, true);             \
+    if (nv == 2 && g_hist_late_hf) ADMMQ_H3L(Q);   \
+    else if (nv == 2) ADMMQ_H3(Q, 2, true);        \
     else ADMMQ_H3(Q, 1, true);                     \
   } else {                                         \
     if (nv == 2) ADMMQ_H3(Q, 2, false);            \
@@ -1423,6 +1470,7 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
     default: ADMMQ_H3N(16); break;
   }
 #undef ADMMQ_H3N
+#undef ADMMQ_H3L
 #undef ADMMQ_H3
 }
 

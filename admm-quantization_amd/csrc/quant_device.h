@@ -416,7 +416,11 @@ __device__ __forceinline__ void split_store4(_Float16* dst_row, int col, float4 
 // The descriptor fields are read once into registers (the stores below would otherwise
 // force their reloads: they go through pointers that may alias the descriptor), element
 // offsets are 32-bit (a problem holds < 2^31 elements: plan_admm), stores are global.
-template <int NT, int NG>
+// STREAM: every input is already in registers (the fused search's finalize): each group is
+// stored as soon as it is computed (no arrays of results live across the groups: the fused
+// search kernel spilled 62 VGPRs holding them); the split form then re-reads its fp32 P for
+// the planes after the row-max barrier. Same float32 / fp64 operations in the same order.
+template <int NT, int NG, bool STREAM = false>
 __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long start, long long end,
                                                     const float4* t4, const float4* u4, const float4* h4,
                                                     const float4* f4, const QParams& qp, int slot, int iter, int rep,
@@ -450,10 +454,77 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
     ADMMQ_FIN_STAMP(4);
   }
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  const int lane = threadIdx.x & 63;
+  if constexpr (STREAM) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the inputs are complete: stores below wait for nothing
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
+      const bool in = e < e32;
+      const int row = e / ld;
+      float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in) {
+        const int c0 = e - row * ld;
+        const float ts[4] = {t4[g].x, t4[g].y, t4[g].z, t4[g].w};
+        const float hs[4] = {h4[g].x, h4[g].y, h4[g].z, h4[g].w}, us[4] = {u4[g].x, u4[g].y, u4[g].z, u4[g].w};
+        const float xs[4] = {ts[0] - us[0], ts[1] - us[1], ts[2] - us[2], ts[3] - us[3]};   // H_T - U
+        const float fs[4] = {f4[g].x, f4[g].y, f4[g].z, f4[g].w};
+        float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
+        gf32x4 hv, uv;
+        float po[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool ok = c0 + k < R;
+          const float hq = mse ? apply_quant_mse(xs[k], qp) : apply_quant(xs[k], qp);
+          const float hn = ok ? hq : 0.f;
+          const float dh = ok ? hn - ts[k] : 0.f;
+          const float un = ok ? us[k] + dh : 0.f;
+          hv[k] = hn; uv[k] = un;
+          po[k] = ok ? fs[k] + rho * (hn + un) : 0.f;
+          const float dp = ok ? hn - hs[k] : 0.f;
+          a1 += dh * dh; a2 += hn * hn; a3 += dp * dp; a4 += un * un;
+        }
+        s1 += (double)a1; s2 += (double)a2; s3 += (double)a3; s4 += (double)a4;
+        pv = make_float4(po[0], po[1], po[2], po[3]);
+        *(gst4*)(Hd + e) = hv;
+        *(gst4*)(Ud + e) = uv;
+        *(gst4*)(Pd + e) = gf32x4{pv.x, pv.y, pv.z, pv.w};   // (split: the planes are formed from it below)
+      }
+      if (split) {   // row max of |next P| per (wave, row), as the non-streaming form
+        const int rg = in ? row : -1;
+        const unsigned mv = in ? __float_as_uint(fmaxf(fmaxf(fabsf(pv.x), fabsf(pv.y)), fmaxf(fabsf(pv.z), fabsf(pv.w))))
+                               : 0u;
+        int r = __builtin_amdgcn_readfirstlane(rg);
+        if (r >= 0) {
+          for (;;) {
+            const unsigned m = wave_max_u32(rg == r ? mv : 0u);
+            if (lane == 0) atomicMax(&rmax[r - row0], m);
+            if (__ballot(rg > r) == 0ull) break;
+            ++r;
+          }
+        }
+      }
+    }
+    ADMMQ_FIN_STAMP(1);
+    if (split) {
+      __syncthreads();
+      ADMMQ_FIN_STAMP(2);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int e = s32 + 4 * (int)threadIdx.x + 4 * NT * g;
+        if (e >= e32) continue;
+        const int row = e / ld;
+        const int c0 = e - row * ld;
+        const float4 pv = *reinterpret_cast<const float4*>(Pd + e);   // this thread's own store
+        const int ex = split_exponent(__uint_as_float(rmax[row - row0]));
+        split_store4(P2 + (size_t)row * 2 * ld, c0, pv, ex);
+        if (c0 == 0) eP[row] = ex;
+      }
+    }
+  } else {
   float4 p4[NG];
   int rows[NG];
   gf32x4 ho[NG], uo[NG];
-  const int lane = threadIdx.x & 63;
   // every group's arithmetic first, then every store: a store issued between two groups
   // would be waited for (vmcnt) by the next group's first register read the compiler
   // cannot prove complete
@@ -527,6 +598,7 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
       if (c0 == 0) eP[row] = ex;
     }
   }
+  }   // (non-streaming form)
   ADMMQ_FIN_STAMP(3);
 #undef ADMMQ_FIN_STAMP
   s1 = wave_sum_f64(s1); s2 = wave_sum_f64(s2);

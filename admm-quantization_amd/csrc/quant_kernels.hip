@@ -5,30 +5,47 @@
 
 namespace admmq {
 
-// Standalone: pack rows x cols -> rows x ld (zero pads) and gather min/max/absmax.
+// Standalone statistics of a tensor (source/quantization.py:72-76: min, max, abs max) and,
+// when cols % 4 != 0, the zero-padded copy rows x ld. One unit = kPackElems elements; each
+// unit's block writes its three partials (plain stores, no same-address atomics: 16 k blocks
+// of one 4096 x 4096 tensor serialized on three words took 565 us); k_qstat folds them.
 __global__ __launch_bounds__(256) void k_qpack(const QJob* __restrict__ jobs, const Chunk* __restrict__ chunks) {
   const Chunk ck = chunks[blockIdx.x];
   const QJob& j = jobs[ck.job];
   const long long total = (long long)j.rows * j.ld;
-  const long long e = (long long)ck.start + 4LL * threadIdx.x;
   unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
-  if (e < total) {
-    const int row = (int)(e / j.ld);
-    const int c0 = (int)(e - (long long)row * j.ld);
-    float v[4];
+  auto acc = [&](float v) {
+    amax = max(amax, __float_as_uint(v) & 0x7FFFFFFFu);
+    mn = min(mn, enc_ord(v));
+    mxo = max(mxo, enc_ord(v));
+  };
+  if (!j.copy) {   // rows are already ld wide (ld == cols): read in place, 16 float4 per thread
+    float4 v[kPackElems / 1024];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = c0 + k;
-      if (c < j.cols) {
-        v[k] = j.src[(size_t)row * j.cols + c];
-        amax = max(amax, __float_as_uint(v[k]) & 0x7FFFFFFFu);
-        mn = min(mn, enc_ord(v[k]));
-        mxo = max(mxo, enc_ord(v[k]));
-      } else {
-        v[k] = 0.f;
-      }
+    for (int k = 0; k < kPackElems / 1024; ++k) {
+      const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * k;
+      v[k] = e < total ? *reinterpret_cast<const float4*>(j.src + e) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    *reinterpret_cast<float4*>(j.Xp + e) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int k = 0; k < kPackElems / 1024; ++k) {
+      const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * k;
+      if (e < total) { acc(v[k].x); acc(v[k].y); acc(v[k].z); acc(v[k].w); }
+    }
+  } else {
+    for (int k = 0; k < kPackElems / 1024; ++k) {
+      const long long e = (long long)ck.start + 4LL * threadIdx.x + 1024LL * k;
+      if (e >= total) break;
+      const int row = (int)(e / j.ld);
+      const int c0 = (int)(e - (long long)row * j.ld);
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + q;
+        v[q] = c < j.cols ? j.src[(size_t)row * j.cols + c] : 0.f;
+        if (c < j.cols) acc(v[q]);
+      }
+      *reinterpret_cast<float4*>(j.Xp + e) = make_float4(v[0], v[1], v[2], v[3]);
+    }
   }
   __shared__ unsigned red[3][4];
   amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
@@ -39,9 +56,30 @@ __global__ __launch_bounds__(256) void k_qpack(const QJob* __restrict__ jobs, co
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       amax = max(amax, red[0][k]); mn = min(mn, red[1][k]); mxo = max(mxo, red[2][k]);
     }
-    atomicMax(&j.mv.stat[0], amax);
-    atomicMin(&j.mv.stat[1], mn);
-    atomicMax(&j.mv.stat[2], mxo);
+    unsigned* o = j.pstat + 3 * (size_t)(blockIdx.x - j.pu0);
+    o[0] = amax; o[1] = mn; o[2] = mxo;
+  }
+}
+
+// one block per tensor: its units' partials -> stat[0..2] (max / min / max: order-free)
+__global__ __launch_bounds__(256) void k_qstat(const QJob* __restrict__ jobs) {
+  const QJob& j = jobs[blockIdx.x];
+  unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
+  for (int u = threadIdx.x; u < j.pun; u += blockDim.x) {
+    amax = max(amax, j.pstat[3 * u + 0]);
+    mn = min(mn, j.pstat[3 * u + 1]);
+    mxo = max(mxo, j.pstat[3 * u + 2]);
+  }
+  __shared__ unsigned red[3][4];
+  amax = wave_max_u32(amax); mn = wave_min_u32(mn); mxo = wave_max_u32(mxo);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = amax; red[1][w] = mn; red[2][w] = mxo; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      amax = max(amax, red[0][k]); mn = min(mn, red[1][k]); mxo = max(mxo, red[2][k]);
+    }
+    j.mv.stat[0] = amax; j.mv.stat[1] = mn; j.mv.stat[2] = mxo;
   }
 }
 
@@ -145,8 +183,9 @@ void launch_channel_quant(const float* x, float* y, long long A, int C, long lon
                      stats, bits, scheme);
 }
 
-void launch_qpack(const QJob* jobs, const Chunk* chunks, int nchunks, hipStream_t s) {
+void launch_qpack(const QJob* jobs, int njobs, const Chunk* chunks, int nchunks, hipStream_t s) {
   if (nchunks > 0) hipLaunchKernelGGL(k_qpack, dim3(nchunks), dim3(256), 0, s, jobs, chunks);
+  if (njobs > 0) hipLaunchKernelGGL(k_qstat, dim3(njobs), dim3(256), 0, s, jobs);
 }
 void launch_qfinal(const QJob* jobs, const Chunk* chunks, int nchunks, int ncand, int bits, int qscheme,
                    hipStream_t s) {

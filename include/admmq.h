@@ -24,6 +24,8 @@
  *                                           squared_relative_diff(W, torch.einsum('ir,jr,kr->ijk', A, B, C))
  *   admmq_lowrank_pre / _post            <- scripts/factorize_lowrank.py:85-101 admm_iteration(H,U,W,H2,proj_func,
  *                                           rho,max_iter,eps): the updates around the projection, device break test
+ *   admmq_panel_xtq / _xy / _outer       <- scripts/factorize_lowrank.py:80-82 (torch.linalg.svd + the rank-r
+ *                                           product): the X^T Q, X Y and U S V^T products of the device projection
  */
 #ifndef ADMMQ_H_
 #define ADMMQ_H_
@@ -252,6 +254,25 @@ int32_t admmq_lowrank_pre(const float* H, const float* U, const float* W, const 
                           int64_t n, float rho, void* workspace, size_t workspace_bytes, void* stream);
 int32_t admmq_lowrank_post(const float* Hn, const float* Hbar, float* H, float* U, int64_t n, float eps,
                            void* workspace, size_t workspace_bytes, void* stream);
+
+/* Panel products of the rank projection (scripts/factorize_lowrank.py:80-82, the truncated
+ * SVD of every low-rank inner step; admmq.lowrank.KrylovProjector builds it from these):
+ *   admmq_panel_xtq    Y = X^T Q  (n x k, row-major, ld k)
+ *   admmq_panel_xy     Z = X Y    (m x k, row-major, ld k)
+ * X: m x n float32 with row stride ldx, read as float32 and widened exactly; Q / Y / Z
+ * float64. v_mfma_f64_16x16x4_f64, fp64 accumulation in a fixed order (the result depends
+ * on m, n, k only). The workspace (admmq_panel_workspace_size, zeroed once before its first
+ * use) holds the cross-workgroup partials and arrival counters; calls on one workspace must
+ * be stream-ordered.
+ *   admmq_panel_outer  O = A B^T  (m x n float32, row stride ldo): A m x r, B n x r float64,
+ * each output summed over r in fp64 and rounded once; r <= 32. */
+size_t admmq_panel_workspace_size(int64_t m, int64_t n, int64_t k);
+int32_t admmq_panel_xtq(const float* X, int64_t m, int64_t n, int64_t ldx, const double* Q, int64_t k, double* Y,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_panel_xy(const float* X, int64_t m, int64_t n, int64_t ldx, const double* Y, int64_t k, double* Z,
+                       void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_panel_outer(const double* A, const double* B, int64_t m, int64_t n, int64_t r, float* O, int64_t ldo,
+                          void* stream);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);

@@ -60,7 +60,7 @@ def main():
     for _ in range(a.svd_sample):
         project_rank(X0 + 1e-3 * torch.randn_like(X0), a.rank)
     torch.cuda.synchronize()
-    svd_s = (time.perf_counter() - t0) / a.svd_sample
+    svd_s = (time.perf_counter() - t0) / a.svd_sample if a.svd_sample > 0 else float("nan")
 
     # the notebook loop with the device projection; inputs of some calls kept for the check
     W_q = torch.randn(*W.shape, generator=g).to(dev)

@@ -109,12 +109,12 @@ def load() -> ctypes.CDLL:
         "admmq_debug_set_gemm_stage": (I32, [I32]),
         "admmq_debug_set_ksplit": (I32, [I32]),
         "admmq_debug_set_ksplit_form": (I32, [I32]),
-        "admmq_debug_set_hist_late_hf": (I32, [I32]),
         "admmq_debug_set_ksplit_balance": (I32, [I32, I32]),
         "admmq_debug_ksplit_balance_count": (ctypes.c_int64, [ctypes.c_void_p, I32]),
         "admmq_debug_ksplit_pieces": (I32, [I32, I32]),
         "admmq_debug_set_even_units": (I32, [I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
+        "admmq_debug_set_fin_nv3": (I32, [I32]),
         "admmq_debug_set_thin_loop": (I32, [I32]),
         "admmq_quantize_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_batched": (I32, [P, I32, I32, I32, I32, P, S, P]),
@@ -145,12 +145,14 @@ def load() -> ctypes.CDLL:
         "admmq_panel_xtq": (I32, [P, I64, I64, I64, P, I64, P, P, S, P]),
         "admmq_panel_xy": (I32, [P, I64, I64, I64, P, I64, P, P, S, P]),
         "admmq_panel_outer": (I32, [P, P, I64, I64, I64, P, I64, P]),
+        "admmq_gram64_workspace_size": (S, [I64, I64, I64]),
+        "admmq_gram64": (I32, [P, I64, P, I64, I64, I64, I64, P, P, S, P]),
         "admmq_version": (I32, []),
         "admmq_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
-        if name.startswith("admmq_debug_") and not hasattr(lib, name):
-            continue   # a diagnostic build (ADMMQ_LIB) from before the switch existed
+        if os.environ.get("ADMMQ_LIB") and not hasattr(lib, name):
+            continue   # a diagnostic build (ADMMQ_LIB) from before the entry point existed
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -254,6 +256,23 @@ class solve_mode:
 
     def __exit__(self, *exc):
         load().admmq_set_solve_mode(self.prev)
+        return False
+
+
+class fin_nv3:
+    """Context manager: let the search take three float4 groups per thread where that keeps
+    the finalize in the search launch (default), or at most two (planned at prepare, so the
+    manager must enclose the whole call). Same integers. Restores the default on exit."""
+
+    def __init__(self, enable: bool):
+        self.enable = enable
+
+    def __enter__(self):
+        load().admmq_debug_set_fin_nv3(1 if self.enable else 0)
+        return self
+
+    def __exit__(self, *exc):
+        load().admmq_debug_set_fin_nv3(1)
         return False
 
 

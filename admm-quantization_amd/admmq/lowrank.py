@@ -75,6 +75,29 @@ class SubspaceProjector:
         return Ur @ torch.diag(S[:r]) @ Vt[:r]
 
 
+def _chol_step(Z: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+    """``Z L^{-T}`` for ``G = L L^T`` (one Cholesky-QR pass: Q = Z R^{-1}, R = L^T)."""
+    L = torch.linalg.cholesky_ex(G)[0]
+    return torch.linalg.solve_triangular(L, Z.T, upper=False).T.contiguous()
+
+
+def orthonormalize(Z: torch.Tensor) -> torch.Tensor:
+    """An orthonormal basis of span(Z) (m x k, float64) by shifted Cholesky QR followed by
+    two plain passes (sCholQR3, Fukaya et al. 2020): three k x k Gram products, Cholesky
+    factors and triangular solves instead of a Householder QR's O(k) launch-bound reflector
+    steps; orthogonal to ~1e-15 for cond(Z) up to ~1e15. The basis differs from the QR's by a
+    k x k rotation (the Krylov subspace, hence the projection, does not). No host sync: a
+    failure shows as a non-orthonormal K at the next Rayleigh-Ritz check, which repairs it."""
+    m, k = Z.shape
+    eye = torch.eye(k, dtype=Z.dtype, device=Z.device)
+    G = panel.gram(Z, Z)
+    shift = 11.0 * (m * k + k * (k + 1)) * 2.0 ** -53 * torch.trace(G)
+    Q = _chol_step(Z, G + shift * eye)
+    for _ in range(2):
+        Q = _chol_step(Q, panel.gram(Q, Q))
+    return Q
+
+
 class KrylovProjector:
     """Rank-``rank`` truncation that matches the exact SVD truncation of
     ``project_rank`` (``scripts/factorize_lowrank.py:80-82``) to ``tol`` on the loop's own
@@ -89,16 +112,21 @@ class KrylovProjector:
     stops when the largest is <= ``tol`` (the truncation then agrees with the exact one to
     about 2 ``tol`` relative: measured on flat spectra, tools/lowrank_bench.py reports it).
     Every pass over X is a hand-written panel kernel (``admmq.panel``: X^T Q, X Y and the
-    final U S V^T, X read as float32 and widened in registers); the re-orthogonalization,
-    the QR of a block and the small eigenproblem are float64 library calls on panels."""
+    final U S V^T, X read as float32 and widened in registers); a new block is
+    orthonormalized by Cholesky QR (``orthonormalize``); the re-orthogonalization and the
+    small eigenproblem are float64 library calls on panels. Each check also measures
+    ||K^T K - I|| (same host sync as the residual) and, past ``ortho_tol``, rebuilds K by a
+    Householder QR and repeats the check."""
 
     def __init__(self, rank: int, block: int = 32, tol: float = 2e-5, check_every: int = 4, max_blocks: int = 64,
-                 seed: int = 0):
+                 seed: int = 0, ortho_tol: float = 1e-9):
         self.rank, self.block, self.tol = rank, block, tol
         self.check_every, self.max_blocks, self.seed = check_every, max_blocks, seed
+        self.ortho_tol = ortho_tol
         self.Q: Optional[torch.Tensor] = None
         self.blocks: List[int] = []
         self.residuals: List[float] = []
+        self.repairs = 0
 
     def __call__(self, X: torch.Tensor) -> torch.Tensor:
         m, n = X.shape
@@ -109,36 +137,47 @@ class KrylovProjector:
         Xf = X.float().contiguous()
         if self.Q is None or self.Q.shape != (m, k):
             g = torch.Generator().manual_seed(self.seed)
-            self.Q = torch.linalg.qr(panel.xy(Xf, torch.randn(n, k, generator=g, dtype=torch.float64).to(X.device)))[0]
+            self.Q = orthonormalize(panel.xy(Xf, torch.randn(n, k, generator=g, dtype=torch.float64).to(X.device)))
         blocks = [self.Q]
         K = self.Q
         Q = self.Q
         res = float("inf")
         nb = 1
+        recheck = False
         while True:
-            if nb >= self.max_blocks or K.shape[1] + k > min(m, n):
+            if recheck or nb >= self.max_blocks or K.shape[1] + k > min(m, n):
                 do_check = True
             else:
                 Z = panel.xy(Xf, panel.xtq(Xf, Q))             # X (X^T Q)
                 for _ in range(2):   # full re-orthogonalization against every block so far
-                    Z = Z - K @ (K.T @ Z)
-                Q = torch.linalg.qr(Z)[0]
+                    Z = Z - K @ panel.gram(K, Z)
+                Q = orthonormalize(Z)
                 blocks.append(Q)
                 K = torch.cat(blocks, 1)
                 nb += 1
                 do_check = nb % self.check_every == 0
             if not do_check:
                 continue
+            recheck = False
             Bt = panel.xtq(Xf, K)                              # B^T = X^T K, n x (nb k)
-            evals, evecs = torch.linalg.eigh(Bt.T @ Bt)        # B B^T, ascending
+            evals, evecs = torch.linalg.eigh(panel.gram(Bt, Bt))   # B B^T, ascending
             idx = torch.arange(evals.shape[0] - 1, evals.shape[0] - 1 - k, -1, device=X.device)   # k <= K's columns
             S = torch.sqrt(torch.clamp(evals[idx], min=0.0))
             Ub = evecs[:, idx]
             U = K @ Ub[:, :r]
             V = (Bt @ Ub[:, :r]) / S[:r]
-            res = float(torch.max(torch.linalg.norm(panel.xy(Xf, V) - U * S[:r], dim=0)) / S[0])
+            res_t = torch.max(torch.linalg.norm(panel.xy(Xf, V) - U * S[:r], dim=0)) / S[0]
+            orth_t = (panel.gram(K, K) - torch.eye(K.shape[1], dtype=K.dtype, device=K.device)).abs().max()
+            res, orth = torch.stack([res_t, orth_t]).tolist()   # one host sync for both
+            if not orth <= self.ortho_tol:   # (NaN included) a block's Cholesky QR failed: rebuild K
+                K = torch.linalg.qr(K)[0]
+                blocks = [K]
+                Q = K[:, -k:]
+                self.repairs += 1
+                recheck = True
+                continue
             if res <= self.tol or nb >= self.max_blocks or K.shape[1] + k > min(m, n):
-                self.Q = torch.linalg.qr(K @ Ub[:, :k])[0]   # warm start: the leading Ritz vectors
+                self.Q = orthonormalize(K @ Ub[:, :k])   # warm start: the leading Ritz vectors
                 self.blocks.append(nb)
                 self.residuals.append(res)
                 if r <= 32:   # the panel kernel's register tile

@@ -15,6 +15,7 @@ import torch
 from . import _lib
 
 _WS: Dict[torch.device, torch.Tensor] = {}
+_GWS: Dict[torch.device, torch.Tensor] = {}
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
@@ -28,7 +29,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def _check_x(X: torch.Tensor) -> torch.Tensor:
-    _lib.require_device(X)
+    if not isinstance(X, torch.Tensor) or X.device.type != "cuda":
+        raise RuntimeError("admmq.panel: X must be a tensor on a ROCm GPU (no CPU implementation)")
     if X.dim() != 2 or X.dtype != torch.float32:
         raise ValueError("admmq.panel: X must be a 2-D float32 device tensor")
     return X if X.stride(1) == 1 else X.contiguous()
@@ -72,7 +74,8 @@ def xy(X: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor] = None) -> 
 
 def outer(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``A B^T`` rounded once to float32 (m x n) for A m x r, B n x r float64, r <= 32."""
-    _lib.require_device(A)
+    if not isinstance(A, torch.Tensor) or not isinstance(B, torch.Tensor) or A.device.type != "cuda" or B.device != A.device:
+        raise RuntimeError("admmq.panel.outer: A and B must be tensors on one ROCm GPU")
     if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[1] or A.dtype != torch.float64 or B.dtype != torch.float64:
         raise ValueError("admmq.panel.outer: A (m x r) and B (n x r) float64 with one r")
     A, B = A.contiguous(), B.contiguous()
@@ -82,3 +85,25 @@ def outer(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) 
     _lib.check(_lib.load().admmq_panel_outer(_lib.ptr(A), _lib.ptr(B), m, n, r, _lib.ptr(O), O.stride(0),
                                              _lib.stream_handle(A.device)), "panel_outer")
     return O
+
+
+def gram(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``A^T B`` (p x q float64) for tall A (m x p) and B (m x q) float64 on one device."""
+    if not isinstance(A, torch.Tensor) or not isinstance(B, torch.Tensor) or A.device.type != "cuda" or B.device != A.device:
+        raise RuntimeError("admmq.panel.gram: A and B must be tensors on one ROCm GPU")
+    if A.dim() != 2 or B.dim() != 2 or A.shape[0] != B.shape[0] or A.dtype != torch.float64 or B.dtype != torch.float64:
+        raise ValueError("admmq.panel.gram: A (m x p) and B (m x q) float64 with one m")
+    A = A if A.stride(1) == 1 else A.contiguous()
+    B = B if B.stride(1) == 1 else B.contiguous()
+    m, p = A.shape
+    q = B.shape[1]
+    C = out if out is not None else torch.empty(p, q, dtype=torch.float64, device=A.device)
+    lib = _lib.load()
+    nb = lib.admmq_gram64_workspace_size(m, p, q)
+    ws = _GWS.get(A.device)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(max(int(nb), 256), dtype=torch.uint8, device=A.device)
+        _GWS[A.device] = ws
+    _lib.check(lib.admmq_gram64(_lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), m, p, q, _lib.ptr(C), _lib.ptr(ws),
+                                ws.numel(), _lib.stream_handle(A.device)), "gram64")
+    return C

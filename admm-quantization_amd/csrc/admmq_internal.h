@@ -225,7 +225,6 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
                  hipEvent_t ev1 = nullptr, bool prefetch_u = false);
 extern int g_gemm_ks_f32;
 extern int g_gemm_f32_stage;   // fp32 64 x 64 staging form (gemm_kernels.hip)
-extern int g_hist_late_hf;     // fused search: finalize loads after the wait (mse_search.hip)
 void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
                       hipStream_t s);
 void launch_gemm_f32p(const ProbDesc* d, const GemmTile* tiles, const int* list_off, int nslots, int slot, int iter,

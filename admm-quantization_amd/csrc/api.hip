@@ -120,6 +120,7 @@ static std::atomic<unsigned> g_fin_wait_polls{kFinWaitPollsDefault};
 // diagnostics: a smaller resident-block budget for the fused finalize (0: the device's),
 // to exercise its several-units-per-block form on small batches
 static std::atomic<int> g_fin_cap_override{0};
+static std::atomic<int> g_fin_nv3{1};   // diagnostics: 0 = never three float4 groups per search thread
 // persistent loop of the thin factors (k_thin_loop) for calls whose problems are all
 // thin: 1 on, 0 off (the per-iteration launches: A/B and cross-check), 2 on with 64-column
 // workgroups wherever allowed (exercises that form on batches that fit without it)
@@ -906,23 +907,33 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   // only the order of the fp64 residual partial sums, never an element's result)
   long long big_elems = 0;
   for (int i : big_jobs) big_elems += (long long)pl.desc[i].I * pl.desc[i].ld;
+  // whole-row units of at most t elements of the big jobs
+  auto big_units = [&](long long t) {
+    long long units = 0;
+    for (int i : big_jobs) {
+      const ProbDesc& d = pl.desc[i];
+      const long long st = d.ld <= t ? (t / d.ld) * d.ld : t;
+      units += ((long long)d.I * d.ld + st - 1) / st;
+    }
+    return units;
+  };
+  // three float4 groups per thread (k_mse_hist3<.., 3, ..>) when the units at two would
+  // outnumber the fused search's resident blocks (2 per CU) and at three would not: the
+  // finalize then stays in the search launch (C4: 5.7 M elements per mode, 722 units of
+  // 8 k against 512 slots; without this, the separate k_finalize_admm launch)
+  if (pl.hist_nv == 2 && g_fin_nv3.load() && big_units((long long)kHistElems * 2) > 2LL * device_cus() &&
+      big_units((long long)kHistElems * 3) <= 2LL * device_cus())
+    pl.hist_nv = 3;
   // (not with hist_nv = 1: a lone layer4 factor's 589 k elements in 512 one-row units
   // instead of 171 three-row ones made its search 22 -> 27 us - the flush atomics and the
   // ticket chain grow with the block count faster than the per-block phases shrink)
   long long hu_big = (long long)kHistElems * pl.hist_nv;
-  if (pl.hist_nv == 2 && g_even_units.load()) {
+  if (pl.hist_nv >= 2 && g_even_units.load()) {
     const long long slots = 2LL * device_cus();
     int big_maxld = 0;
     for (int i : big_jobs) big_maxld = std::max(big_maxld, pl.desc[i].ld);
-    for (long long t = std::max<long long>(big_maxld, (big_elems + slots - 1) / slots); t < hu_big; t += 256) {
-      long long units = 0;
-      for (int i : big_jobs) {
-        const ProbDesc& d = pl.desc[i];
-        const long long st = d.ld <= t ? (t / d.ld) * d.ld : t;
-        units += ((long long)d.I * d.ld + st - 1) / st;
-      }
-      if (units <= slots) { hu_big = t; break; }
-    }
+    for (long long t = std::max<long long>(big_maxld, (big_elems + slots - 1) / slots); t < hu_big; t += 256)
+      if (big_units(t) <= slots) { hu_big = t; break; }
   }
   // stage-1 / finalize units of the small jobs (I <= kThinRows) go last: when their
   // fused one-block path runs (k_mse_small_admm), the launches take only the others
@@ -1022,7 +1033,7 @@ static unsigned long long plan_fingerprint(const AdmmPlan& pl, const void* ws) {
     mix(d.I); mix(d.R); mix(d.Ip); mix(d.ld); mix(d.ldm); mix(d.split); mix(d.ksplit);
     mix(off(d.Fp)); mix(off(d.M)); mix(off(d.P2)); mix(off(d.kpart)); mix(off(d.mv.h1)); mix(off(d.flags));
   }
-  mix(off(pl.d_desc)); mix(off(pl.d_tiles)); mix(off(pl.d_kctr)); mix(off(pl.d_rank0));
+  mix(off(pl.d_desc)); mix(off(pl.d_tiles)); mix(off(pl.d_kctr)); mix(off(pl.d_rank0)); mix(pl.hist_nv);
   return h;
 }
 
@@ -1229,6 +1240,14 @@ size_t admmq_debug_admm_plan_bytes(const admmq_problem* probs, int32_t nprob, in
   return pl.bytes;
 }
 
+// diagnostics (not in include/admmq.h): 1 (default) = the search takes three float4 groups
+// per thread where that keeps the finalize fused (planned at prepare), 0 = at most two
+int32_t admmq_debug_set_fin_nv3(int32_t on) {
+  if (on < 0 || on > 1) return fail(ADMMQ_ERR_ARG, "fin_nv3 must be 0 or 1");
+  g_fin_nv3 = on;
+  return ADMMQ_OK;
+}
+
 // diagnostics (not in include/admmq.h): resident-block budget of the fused finalize (0: the device's)
 int32_t admmq_debug_set_fin_capacity(int32_t blocks) {
   if (blocks < 0) return fail(ADMMQ_ERR_ARG, "blocks must be >= 0");
@@ -1315,13 +1334,6 @@ int64_t admmq_debug_ksplit_balance_count(const int32_t* IR, int32_t nprob) {
     }
   }
   return ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
-}
-// diagnostics: the fused search's finalize loads (H, F) issued after the wait for the job's
-// selection (1) instead of before it (0, default); same results
-int32_t admmq_debug_set_hist_late_hf(int32_t on) {
-  if (on < 0 || on > 1) return fail(ADMMQ_ERR_ARG, "late_hf must be 0 or 1");
-  g_hist_late_hf = on;
-  return ADMMQ_OK;
 }
 // diagnostics: the K-split pieces the planner gives an (I, R) factor (0 on bad arguments)
 int32_t admmq_debug_ksplit_pieces(int32_t I, int32_t R) {

@@ -126,14 +126,27 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_post(const float* __restrict_
     last = old + 1 == (int)gridDim.x;
   }
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
+  if (!last) return;
+  // the last block sums the partials in a fixed order: thread t the blocks t, t + 256, ...
+  // ascending, then the wave sums and the four waves in order (one thread walking all
+  // 4 x 1024 partials took ~200 us of dependent loads)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double t[4] = {0.0, 0.0, 0.0, 0.0};
-  for (unsigned b = 0; b < gridDim.x; ++b)
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += kLrThreads)
+#pragma unroll
     for (int k = 0; k < 4; ++k) t[k] += __hip_atomic_load(part + 4 * (size_t)b + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = lr_wave_sum(t[k]);
+  __syncthreads();   // (red is reused)
+  if (lane == 0) { red[0][w] = t[0]; red[1][w] = t[1]; red[2][w] = t[2]; red[3][w] = t[3]; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double u[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < kLrThreads / 64; ++q)
+    for (int k = 0; k < 4; ++k) u[k] += red[k][q];
   st->ticket = 0;
   st->iters += 1;
-  if (t[0] / t[1] < (double)eps && t[2] / t[3] < (double)eps) st->done = 1;
+  if (u[0] / u[1] < (double)eps && u[2] / u[3] < (double)eps) st->done = 1;
 }
 
 static size_t lr_bytes() { return 256 + (size_t)kLrBlocks * 4 * sizeof(double); }

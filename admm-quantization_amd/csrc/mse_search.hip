@@ -505,71 +505,6 @@ __device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned lon
 }
 
 
-// The same selection by ONE wave for n <= 256 (the last stage-1 block of a job): lane l owns
-// candidates 4l .. 4l + 3, sums their kHistRep replicas straight from the job's global
-// histograms (sc1 atomic loads), computes their bounds (the same fp64 operations per
-// candidate as select_block, so the same S), the wave min of A + E and the ascending list
-// by a wave prefix count - no block barrier until the final one (lsel visible to every
-// thread). Called by every thread of the block.
-__device__ void select_wave4(const MseView& v, int* sel, int* lsel, const unsigned long long* G1,
-                             const unsigned long long* G2, int slot, float mx, int n, int qmax) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    unsigned long long t1[4], t2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { t1[j] = 0ull; t2[j] = 0ull; }
-#pragma unroll
-    for (int r = 0; r < kHistRep; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = 4 * lane + j;
-        if (c < n) {
-          t1[j] += __hip_atomic_load((gu64*)&G1[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          t2[j] += __hip_atomic_load((gu64*)&G2[r * (n + 1) + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    SelCtx cx;
-    cx.S2 = S2; cx.mx = mx; cx.n = n; cx.denf = (float)(2 * qmax - 1);
-    cx.u = 0x1p-24;
-    cx.fixu = ldexp(1.0, -hist_fixed_exp(mx, v.nelem, qmax));
-    cx.Kterm = (double)v.nq * ldexp(1.0, -fixed_exp(mx, v.nq));
-    cx.Nterm = (double)((long long)v.nelem * qmax);
-    cx.tiny = 8.0 * (double)v.nelem * 0x1p-149;
-    double lo[4], hi[4], hmin = 1e300;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 4 * lane + j;
-      lo[j] = hi[j] = 1e300;
-      if (c < n) cx.bounds(c, t1[j], t2[j], lo[j], hi[j]);
-      hmin = fmin(hmin, hi[j]);
-    }
-    const double mn = wave_min_f64(hmin);
-    unsigned cnt = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cnt += (4 * lane + j < n && lo[j] <= mn) ? 1u : 0u;
-    const unsigned suf = wave_suffix_u32(cnt);                   // keeps in lanes >= this one
-    const int total = (int)__builtin_amdgcn_readfirstlane(suf);   // lane 0: all of them
-    int pos = total - (int)suf;                                    // keeps in lanes below
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 4 * lane + j;
-      if (c < n && lo[j] <= mn) {
-        if (pos < kMaxSel) { sel[2 + pos] = c; lsel[2 + pos] = c; }
-        ++pos;
-      }
-    }
-    if (lane == 0) {
-      if (total > kMaxSel || total == 0) { sel[0] = n; sel[1] = -1; }
-      else { sel[0] = total; sel[1] = 0; }
-      lsel[0] = sel[0]; lsel[1] = sel[1];
-      if (ADMMQ_TRACE) atomicAdd(&g_sel_stats[(total == 1) ? 0 : ((total > kMaxSel || total == 0) ? 2 : 1)], 1ull);
-    }
-  }
-  __syncthreads();
-}
-
 // Rank-by-counting of the thresholds (fallback when the host order does not hold):
 // rows thr[j][.] are non-decreasing; with the order (value, level, candidate)
 // rank(k, c) = sum_{j<k} #{row j <= T} + c + sum_{j>k} #{row j < T}, L = sum_j #{row j <= T}.
@@ -938,14 +873,14 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
 // with a stale selection record; the caller re-runs the call with the separate finalize
 // launch (the PyTorch op does). Saves the finalize launch, its dependent parameter chain
 // and its re-read of H_T and U.
-// LATE (FIN only): the finalize's H / F loads are issued after the wait for the job's
-// selection instead of before it (fewer registers live across the wait, one more load
-// latency on the finalize path)
 #ifndef ADMMQ_FIN_STREAM
 #define ADMMQ_FIN_STREAM 1
 #endif
 constexpr bool kFinStream = ADMMQ_FIN_STREAM != 0;   // the fused finalize stores each group at once
-template <int QMAX, int NV, bool FIN, bool LATE = false>
+// NV = 3 (FIN: the launches whose units would not all be resident at 2 groups per thread,
+// e.g. C4): U is re-read with H and F for the finalize instead of held across the search
+// (its registers are what would spill), an L2 hit written by the solve's epilogue.
+template <int QMAX, int NV, bool FIN>
 __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     const ProbDesc* __restrict__ d, const QJob* __restrict__ qj, const Chunk* __restrict__ chunks, int ncand, int slot,
     const unsigned short* __restrict__ rank0, const unsigned short* __restrict__ groups, int ngroups, int bits,
@@ -961,6 +896,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   H3Pre pre;
   h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kH3Threads);
   asm volatile("" ::: "memory");   // issue order: the loads above before the element loads
+  constexpr bool kReloadU = FIN && NV >= 3;
   float4 x4[2 * NV], u4[2 * NV], h4[FIN ? 2 * NV : 1], f4[FIN ? 2 * NV : 1];
 #pragma unroll
   for (int hh = 0; hh < 2 * NV; ++hh) {   // 8 NV elements: float4 hh at start + 4 tid + 2048 hh
@@ -991,6 +927,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
 #pragma unroll
     for (int hh = 0; hh < 2 * NV; ++hh) {
       const long long ec = (long long)ck.start + 4LL * threadIdx.x + 2048LL * hh;
+      if constexpr (kReloadU) u4[hh] = gld4(ck.U + (ec < total ? ec : 0));
       h4[hh] = gld4(ck.H + (ec < total ? ec : 0));
       f4[hh] = gld4(ck.F + (ec < total ? ec : 0));
     }
@@ -1100,9 +1037,10 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const unsigned long long* G1 = v.h1 + (size_t)slot * kHistRep * (n + 1);
     const unsigned long long* G2 = v.h2 + (size_t)slot * kHistRep * (n + 1);
-    if (n <= 256) {
-      select_wave4(v, sel, lsel, G1, G2, slot, mx, n, QMAX);
-    } else if (n <= (int)blockDim.x) {
+    // (a one-wave form - lane l summing candidates 4l .. 4l + 3 over the kHistRep replicas
+    // itself - made the other blocks' wait for this selection 8.0 -> 16.8 us at C3: 64
+    // dependent sc1 loads per lane against 16 per thread here)
+    if (n <= (int)blockDim.x) {
       const int c = threadIdx.x;
       unsigned long long t1 = 0ull, t2 = 0ull;
       if (c < n) {
@@ -1151,7 +1089,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   }
   if constexpr (FIN) {
     const ProbDesc& p = d[ck.job];
-    if (!LATE) load_hf();
+    load_hf();
     if (!last) {   // wait for the job's selection (bounded)
       if (threadIdx.x == 0) {
         unsigned polls = 0;
@@ -1174,7 +1112,6 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
         return;
       }
     }
-    if (LATE) load_hf();
     QParams qp;
     if (lsel[0] == 1) {
       qp = qparams_mse(bits, cand_t(mx, lsel[2], n));
@@ -1425,7 +1362,7 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
   const int abl = 0;
 #define ADMMQ_H1(Q, V) \
   hipLaunchKernelGGL((k_mse_hist<Q, V>), dim3(nchunks), dim3(1024), lds, s, d, q, chunks, ncand, slot, abl)
-#define ADMMQ_H1N(Q) if (nv == 2) ADMMQ_H1(Q, 2); else ADMMQ_H1(Q, 1)
+#define ADMMQ_H1N(Q) if (nv == 3) ADMMQ_H1(Q, 3); else if (nv == 2) ADMMQ_H1(Q, 2); else ADMMQ_H1(Q, 1)
   switch (bits) {
     case 1: ADMMQ_H1N(1); break;
     case 2: ADMMQ_H1N(2); break;
@@ -1440,7 +1377,6 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
 bool merged_ok(int ncand, int bits) {
   return ncand >= 2 && ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist3_lds_bytes(ncand, bits) <= 150 * 1024;
 }
-int g_hist_late_hf = 0;   // fused search: the finalize's H / F loads after the wait (k_mse_hist3 LATE)
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
                       unsigned wait_polls, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -1450,16 +1386,14 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
 #define ADMMQ_H3(Q, V, F)                                                                                         \
   hipExtLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, chunks, \
                         ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
-#define ADMMQ_H3L(Q)                                                                                               \
-  hipExtLaunchKernelGGL((k_mse_hist3<Q, 2, true, true>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, \
-                        chunks, ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
 #define ADMMQ_H3N(Q)                               \
   if (fin) {                                       \
-    if (nv == 2 && g_hist_late_hf) ADMMQ_H3L(Q);   \
+    if (nv == 3) ADMMQ_H3(Q, 3, true);             \
     else if (nv == 2) ADMMQ_H3(Q, 2, true);        \
     else ADMMQ_H3(Q, 1, true);                     \
   } else {                                         \
-    if (nv == 2) ADMMQ_H3(Q, 2, false);            \
+    if (nv == 3) ADMMQ_H3(Q, 3, false);            \
+    else if (nv == 2) ADMMQ_H3(Q, 2, false);       \
     else ADMMQ_H3(Q, 1, false);                    \
   }
   switch (bits) {
@@ -1470,7 +1404,6 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
     default: ADMMQ_H3N(16); break;
   }
 #undef ADMMQ_H3N
-#undef ADMMQ_H3L
 #undef ADMMQ_H3
 }
 
@@ -1496,8 +1429,9 @@ int hist3_fin_capacity(int ncand, int bits, int nv) {
   int per = 0;
   hipError_t e = hipErrorInvalidValue;
 #define ADMMQ_OCC(Q) \
-  e = nv == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 2, true>, kH3Threads, lds) \
-              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 1, true>, kH3Threads, lds)
+  e = nv == 3   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 3, true>, kH3Threads, lds) \
+      : nv == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 2, true>, kH3Threads, lds) \
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 1, true>, kH3Threads, lds)
   switch (bits) {
     case 1: ADMMQ_OCC(1); break;
     case 2: ADMMQ_OCC(2); break;

@@ -46,7 +46,8 @@ __device__ __forceinline__ f64x4p pan_mfma(double a, double b, f64x4p c) {
 }
 
 // In-workgroup sum of the 4 waves' tiles (wave order), then the cross-workgroup hand-off.
-// Returns true in wave 0 of the workgroup that holds the final sum in acc.
+// Returns true in wave 0 of the workgroup that holds the final sum in acc. ctr: the END of
+// the counter array (tile t counts at ctr[-1 - t]).
 __device__ __forceinline__ bool pan_combine(f64x4p (&acc)[4][2], double* part, unsigned* ctr, int tile) {
   __shared__ double red[3][32][64];   // 48 KB: [wave - 1][value][lane] (lane-contiguous: no conflicts)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -86,7 +87,7 @@ __device__ __forceinline__ bool pan_combine(f64x4p (&acc)[4][2], double* part, u
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int last = 0;
     if (lane == 0) {
-      const unsigned old = __hip_atomic_fetch_add(ctr + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(ctr - 1 - tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = ((old + 1u) % (unsigned)kPanG) == 0u ? 1 : 0;
     }
     if (!__builtin_amdgcn_readfirstlane(last)) return false;   // (lane 0 is active: its value)
@@ -270,18 +271,20 @@ __global__ __launch_bounds__(256, 2) void k_panel_xy(const float* __restrict__ X
 }
 
 // O = A B^T rounded to float32 once: thread (j4 = 4 columns) x 16 rows, B rows of its columns
-// held in registers, the A row broadcast. grid (ceil(n / 1024), ceil(m / 16)), 256 threads.
+// held in registers (RB = r rounded up to 8, 16 or 32: compile-time trip counts, so the
+// rows stay in VGPRs), the A row broadcast. grid (ceil(n / 1024), ceil(m / 16)), 256 threads.
 constexpr int kOuterRows = 16;
 constexpr int kOuterMaxR = 32;
+template <int RB>
 __global__ __launch_bounds__(256) void k_panel_outer(const double* __restrict__ A, const double* __restrict__ B,
                                                      int m, int n, int r, float* __restrict__ O, int ldo) {
   const int j = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (j >= n) return;
-  double bj[4][kOuterMaxR];
+  double bj[4][RB];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int c = 0; c < kOuterMaxR; ++c) bj[q][c] = (c < r && j + q < n) ? B[(size_t)(j + q) * r + c] : 0.0;
+    for (int c = 0; c < RB; ++c) bj[q][c] = (c < r && j + q < n) ? B[(size_t)(j + q) * r + c] : 0.0;
   const int i0 = blockIdx.y * kOuterRows;
   for (int ii = 0; ii < kOuterRows; ++ii) {
     const int i = i0 + ii;
@@ -289,9 +292,8 @@ __global__ __launch_bounds__(256) void k_panel_outer(const double* __restrict__ 
     const double* ar = A + (size_t)i * r;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int c = 0; c < kOuterMaxR; ++c) {
-      if (c >= r) break;
-      const double a = ar[c];
+    for (int c = 0; c < RB; ++c) {
+      const double a = c < r ? ar[c] : 0.0;   // (c >= r: b = 0 too, so the sum is unchanged)
 #pragma unroll
       for (int q = 0; q < 4; ++q) s[q] = fma(a, bj[q][c], s[q]);
     }
@@ -306,13 +308,99 @@ __global__ __launch_bounds__(256) void k_panel_outer(const double* __restrict__ 
   }
 }
 
+// C = A^T B (p x q, float64) for tall A (m x p) and B (m x q): the Gram / cross products of
+// the Krylov panels (Z^T Z of a block's Cholesky QR, K^T Z of the re-orthogonalization,
+// B B^T of the Rayleigh-Ritz step). A wave owns a 32 x 32 tile (2 x 2 MFMA tiles) over
+// m / (4 S) rows, the 4 waves of a workgroup consecutive row ranges (summed in wave order
+// in LDS); grid (tiles, S); k_gram64_sum adds the S workgroup partials in order. Library
+// GEMMs ran these (m = 4096, p = q = 32) on one workgroup: ~220 us each.
+constexpr int kGramMaxS = 64;
+__global__ __launch_bounds__(256) void k_gram64(const double* __restrict__ A, int lda, const double* __restrict__ B,
+                                                int ldb, int m, int p, int q, double* __restrict__ part) {
+  __shared__ double red[3][16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int tq = (q + 31) / 32;
+  const int p0 = (blockIdx.x / tq) * 32, q0 = (blockIdx.x % tq) * 32;
+  const int S = gridDim.y;
+  const int steps = (m + 3) >> 2;
+  const int per = (steps + 4 * S - 1) / (4 * S);
+  const int s0 = min(steps, (blockIdx.y * 4 + w) * per), s1 = min(steps, s0 + per);
+  f64x4p acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[a][u] = f64x4p{0.0, 0.0, 0.0, 0.0};
+  for (int st = s0; st < s1; ++st) {
+    const int i = 4 * st + fk;
+    double av[2], bv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int pc = p0 + 16 * t + fr, qc = q0 + 16 * t + fr;
+      av[t] = (i < m && pc < p) ? A[(size_t)i * lda + pc] : 0.0;
+      bv[t] = (i < m && qc < q) ? B[(size_t)i * ldb + qc] : 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[a][u] = pan_mfma(av[a], bv[u], acc[a][u]);
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) red[w - 1][(a * 2 + u) * 4 + v][lane] = acc[a][u][v];
+  }
+  __syncthreads();
+  if (w != 0) return;
+  double* o = part + ((size_t)blockIdx.x * S + blockIdx.y) * 16 * 64;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int x = (a * 2 + u) * 4 + v;
+        o[x * 64 + lane] = ((acc[a][u][v] + red[0][x][lane]) + red[1][x][lane]) + red[2][x][lane];
+      }
+}
+
+// one wave per tile: the S partials in order, then the D map (row (lane >> 4) + 4 v of the
+// p-tile a, column lane & 15 of the q-tile u)
+__global__ __launch_bounds__(64) void k_gram64_sum(const double* __restrict__ part, int S, int p, int q,
+                                                   double* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x;
+  const int tq = (q + 31) / 32;
+  const int p0 = (blockIdx.x / tq) * 32, q0 = (blockIdx.x % tq) * 32;
+  const double* src = part + (size_t)blockIdx.x * S * 16 * 64;
+#pragma unroll
+  for (int x = 0; x < 16; ++x) {
+    double sum = src[x * 64 + lane];
+    for (int g = 1; g < S; ++g) sum += src[((size_t)g * 16 + x) * 64 + lane];
+    const int a = x >> 3, u = (x >> 2) & 1, v = x & 3;
+    const int r = p0 + 16 * a + (lane >> 4) + 4 * v, c = q0 + 16 * u + (lane & 15);
+    if (r < p && c < q) C[(size_t)r * ldc + c] = sum;
+  }
+}
+
+static int gram_slices(int64_t m) { return (int)std::max<int64_t>(1, std::min<int64_t>(kGramMaxS, (m + 255) / 256)); }
+static size_t gram_bytes(int64_t m, int64_t p, int64_t q) {
+  return (size_t)((p + 31) / 32) * (size_t)((q + 31) / 32) * gram_slices(m) * 16 * 64 * sizeof(double);
+}
+
 static size_t pan_align(size_t v) { return (v + 255) / 256 * 256; }
 
 static size_t pan_tiles(int64_t rows, int64_t k) { return (size_t)((rows + 63) / 64) * (size_t)((k + 31) / 32); }
 
+// Workspace: the partials from offset 0, the arrival counters at the END, counter t at
+// end - 4 (t + 1): a tile's counter has the same address in every call on the workspace
+// whatever the call's tile count (a later call with more tiles extends the counter region
+// downwards, into bytes no call's partials reach: every call checks partials + counters fit).
 static size_t pan_bytes(int64_t m, int64_t n, int64_t k) {
   const size_t tiles = std::max(pan_tiles(m, k), pan_tiles(n, k));
-  return 256 + pan_align(tiles * sizeof(unsigned)) + tiles * kPanG * 64 * 32 * sizeof(double);
+  return tiles * kPanG * 64 * 32 * sizeof(double) + pan_align(tiles * sizeof(unsigned));
 }
 
 static int pan_args(const float* X, int64_t m, int64_t n, int64_t ldx, const double* P, int64_t k, const double* Out,
@@ -337,9 +425,8 @@ size_t admmq_panel_workspace_size(int64_t m, int64_t n, int64_t k) {
 int32_t admmq_panel_xtq(const float* X, int64_t m, int64_t n, int64_t ldx, const double* Q, int64_t k, double* Y,
                         void* workspace, size_t workspace_bytes, void* stream) {
   if (const int rc = pan_args(X, m, n, ldx, Q, k, Y, workspace, workspace_bytes)) return rc;
-  unsigned* ctr = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + 256);
-  const size_t tiles = std::max(pan_tiles(m, k), pan_tiles(n, k));
-  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256 + pan_align(tiles * sizeof(unsigned)));
+  unsigned* ctr = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + (workspace_bytes & ~(size_t)3));
+  double* part = static_cast<double*>(workspace);
   const dim3 grid((unsigned)((n + 63) / 64), kPanG, (unsigned)((k + 31) / 32));
   const bool v4 = n % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -353,9 +440,8 @@ int32_t admmq_panel_xtq(const float* X, int64_t m, int64_t n, int64_t ldx, const
 int32_t admmq_panel_xy(const float* X, int64_t m, int64_t n, int64_t ldx, const double* Y, int64_t k, double* Z,
                        void* workspace, size_t workspace_bytes, void* stream) {
   if (const int rc = pan_args(X, m, n, ldx, Y, k, Z, workspace, workspace_bytes)) return rc;
-  unsigned* ctr = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + 256);
-  const size_t tiles = std::max(pan_tiles(m, k), pan_tiles(n, k));
-  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256 + pan_align(tiles * sizeof(unsigned)));
+  unsigned* ctr = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + (workspace_bytes & ~(size_t)3));
+  double* part = static_cast<double*>(workspace);
   const dim3 grid((unsigned)((m + 63) / 64), kPanG, (unsigned)((k + 31) / 32));
   const bool v4 = n % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -366,14 +452,38 @@ int32_t admmq_panel_xy(const float* X, int64_t m, int64_t n, int64_t ldx, const 
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "panel_xy: launch failed");
 }
 
+size_t admmq_gram64_workspace_size(int64_t m, int64_t p, int64_t q) {
+  return (m <= 0 || p <= 0 || q <= 0) ? 0 : gram_bytes(m, p, q);
+}
+
+int32_t admmq_gram64(const double* A, int64_t lda, const double* B, int64_t ldb, int64_t m, int64_t p, int64_t q,
+                     double* C, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!A || !B || !C || m <= 0 || p <= 0 || q <= 0 || lda < p || ldb < q)
+    return set_error(ADMMQ_ERR_ARG, "gram64: bad arguments");
+  if (m >= (1LL << 31) || p > 8192 || q > 8192) return set_error(ADMMQ_ERR_ARG, "gram64: sizes out of range");
+  if (!workspace || workspace_bytes < gram_bytes(m, p, q)) return set_error(ADMMQ_ERR_WORKSPACE, "gram64: workspace too small");
+  const int S = gram_slices(m);
+  const unsigned tiles = (unsigned)(((p + 31) / 32) * ((q + 31) / 32));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  double* part = static_cast<double*>(workspace);
+  hipLaunchKernelGGL(k_gram64, dim3(tiles, S), dim3(256), 0, s, A, (int)lda, B, (int)ldb, (int)m, (int)p, (int)q, part);
+  hipLaunchKernelGGL(k_gram64_sum, dim3(tiles), dim3(64), 0, s, part, S, (int)p, (int)q, C, (int)q);
+  return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "gram64: launch failed");
+}
+
 int32_t admmq_panel_outer(const double* A, const double* B, int64_t m, int64_t n, int64_t r, float* O, int64_t ldo,
                           void* stream) {
   if (!A || !B || !O || m <= 0 || n <= 0 || r <= 0 || ldo < n) return set_error(ADMMQ_ERR_ARG, "panel_outer: bad arguments");
   if (r > kOuterMaxR) return set_error(ADMMQ_ERR_ARG, "panel_outer: rank above 32");
   if (m >= (1LL << 31) || n >= (1LL << 31)) return set_error(ADMMQ_ERR_ARG, "panel_outer: sizes out of range");
   const dim3 grid((unsigned)((n + 1023) / 1024), (unsigned)((m + kOuterRows - 1) / kOuterRows));
-  hipLaunchKernelGGL(k_panel_outer, grid, dim3(256), 0, static_cast<hipStream_t>(stream), A, B, (int)m, (int)n, (int)r, O,
-                     (int)ldo);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (r <= 8)
+    hipLaunchKernelGGL(k_panel_outer<8>, grid, dim3(256), 0, s, A, B, (int)m, (int)n, (int)r, O, (int)ldo);
+  else if (r <= 16)
+    hipLaunchKernelGGL(k_panel_outer<16>, grid, dim3(256), 0, s, A, B, (int)m, (int)n, (int)r, O, (int)ldo);
+  else
+    hipLaunchKernelGGL(k_panel_outer<32>, grid, dim3(256), 0, s, A, B, (int)m, (int)n, (int)r, O, (int)ldo);
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "panel_outer: launch failed");
 }
 

@@ -406,6 +406,7 @@ def emulate_shards(a):
     _lib.check(lib.admmq_debug_set_ksplit(a.ksplit), "ksplit")
     _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
     _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
+    _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
     N = a.emulate_world
     full, _, _ = build_workload(a.model, 0, 1, "layers", device)
     full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
@@ -468,8 +469,9 @@ def main():
                          "the launch's CU-level LPT makespan (a parallel piece priced COST K-steps extra); same bits")
     ap.add_argument("--gemm-stage", type=int, default=-1,
                     help="A/B: fp32 64x64 staging form 0..4 (library default 3; 2 = 2-deep ring, 4 tiles per CU)")
-    ap.add_argument("--late-hf", type=int, default=0, choices=[0, 1],
-                    help="A/B: the fused search's finalize loads of H and F after the wait for the selection")
+    ap.add_argument("--fin-nv3", type=int, default=1, choices=[0, 1],
+                    help="A/B: 1 (library default) = three float4 groups per search thread where that keeps the "
+                         "finalize in the search launch (C4), 0 = at most two (separate finalize launch at C4)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
@@ -496,7 +498,7 @@ def main():
     _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
     if a.gemm_stage >= 0:
         _lib.check(lib.admmq_debug_set_gemm_stage(a.gemm_stage), "gemm_stage")
-    _lib.check(lib.admmq_debug_set_hist_late_hf(a.late_hf), "late_hf")
+    _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
     if a.f32_kernel >= 0:
         _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")
     split = a.solve == "split"

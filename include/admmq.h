@@ -262,8 +262,9 @@ int32_t admmq_lowrank_post(const float* Hn, const float* Hbar, float* H, float* 
  * X: m x n float32 with row stride ldx, read as float32 and widened exactly; Q / Y / Z
  * float64. v_mfma_f64_16x16x4_f64, fp64 accumulation in a fixed order (the result depends
  * on m, n, k only). The workspace (admmq_panel_workspace_size, zeroed once before its first
- * use) holds the cross-workgroup partials and arrival counters; calls on one workspace must
- * be stream-ordered.
+ * use) holds the cross-workgroup partials and, at its end, the arrival counters: calls on
+ * one workspace must be stream-ordered and pass the same workspace_bytes (a larger
+ * workspace for larger panels is a new, zeroed buffer).
  *   admmq_panel_outer  O = A B^T  (m x n float32, row stride ldo): A m x r, B n x r float64,
  * each output summed over r in fp64 and rounded once; r <= 32. */
 size_t admmq_panel_workspace_size(int64_t m, int64_t n, int64_t k);
@@ -273,6 +274,12 @@ int32_t admmq_panel_xy(const float* X, int64_t m, int64_t n, int64_t ldx, const 
                        void* workspace, size_t workspace_bytes, void* stream);
 int32_t admmq_panel_outer(const double* A, const double* B, int64_t m, int64_t n, int64_t r, float* O, int64_t ldo,
                           void* stream);
+/* C = A^T B (p x q, row-major, ld q) for tall float64 A (m x p, row stride lda) and B (m x q,
+ * row stride ldb): the panels' Gram / cross products (fixed summation order; the workspace,
+ * admmq_gram64_workspace_size, needs no initialisation). */
+size_t admmq_gram64_workspace_size(int64_t m, int64_t p, int64_t q);
+int32_t admmq_gram64(const double* A, int64_t lda, const double* B, int64_t ldb, int64_t m, int64_t p, int64_t q,
+                     double* C, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);

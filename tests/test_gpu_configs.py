@@ -134,6 +134,30 @@ def test_c4_batched_equals_single(torch_dev):
     _batched_equals_single(torch, dev, probs[::3], iters=3)
 
 
+def test_c4_fused_three_groups_equals_separate(torch_dev):
+    """C4 mode 0 (all 48 resnet50 factors, 5.7 M elements): too many 8 k-element search
+    units for one resident round, so the search takes three float4 groups per thread
+    (k_mse_hist3<.., 3, true>: U re-read for the finalize) and keeps the finalize fused. Its
+    H, U and iteration counts equal those of two groups per thread with the separate
+    k_finalize_admm launch, bit for bit, with no internal fault."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched, _lib
+    probs = _config_problems("resnet50", 0)
+
+    def run(nv3, fused):
+        ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+              for (_, H, F, G) in probs]
+        with _lib.fin_nv3(nv3), _lib.fused_finalize(fused):
+            Hs, info = admm_iteration_batched(ps, 4, 0.0, 4, MSE, return_info=True)
+        return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
+
+    a, ia = run(True, True)
+    b, ib = run(False, False)
+    assert (ia[:, 3] == 0).all() and (ia[:, 4] == 0).all() and np.array_equal(ia[:, :3], ib[:, :3])
+    for (ha, ua), (hb, ub), pr in zip(a, b, probs):
+        assert np.array_equal(_bits(ha), _bits(hb)) and np.array_equal(_bits(ua), _bits(ub)), pr[0]
+
+
 def _llama_problem(torch, dev, I, J, R, seed):
     """2-way mode 0 of W (I, J): F = W B, G = B^T B (scripts/factorize.py:276-277)."""
     g = torch.Generator().manual_seed(seed)

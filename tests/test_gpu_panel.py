@@ -77,6 +77,25 @@ def test_strided_x_and_xxtq_chain(env):
         assert _colrel(Z, Xd @ (Xd.T @ Q)) < 1e-12
 
 
+def test_tile_count_grows_on_one_workspace(env):
+    """Calls whose tile counts grow (k = 32, then the Rayleigh-Ritz panel of 8 blocks, then
+    back) on one workspace: every tile's arrival counter keeps its address (the counters sit
+    at the workspace's end), so a later, larger call never reads a partial as a counter."""
+    torch, dev = env
+    from admmq import panel
+    g = torch.Generator(device="cpu").manual_seed(9)
+    X = torch.randn(2048, 2048, generator=g).to(dev)
+    Xd = X.double()
+    lib = __import__("admmq")._lib.load()
+    ws = torch.zeros(lib.admmq_panel_workspace_size(2048, 2048, 256), dtype=torch.uint8, device=dev)
+    panel._WS[X.device] = ws   # one workspace for every call below
+    for k in (32, 256, 64, 256, 32, 160):
+        Q = torch.randn(2048, k, generator=g, dtype=torch.float64).to(dev)
+        assert _colrel(panel.xtq(X, Q), Xd.T @ Q) < 1e-13
+        assert _colrel(panel.xy(X, Q), Xd @ Q) < 1e-13
+    assert panel._WS[X.device] is ws
+
+
 @pytest.mark.parametrize("m,n,r", [(4096, 4096, 8), (1000, 777, 32), (17, 5, 3)])
 def test_outer_rounds_once(env, m, n, r):
     torch, dev = env
@@ -91,6 +110,23 @@ def test_outer_rounds_once(env, m, n, r):
     err = (O.double() - ref).abs()
     bound = 2.0 ** -24 * ref.abs() + 1e-13 * (A.abs() @ B.abs().T)
     assert bool((err <= bound).all())
+
+
+@pytest.mark.parametrize("m,p,q", [(4096, 32, 32), (4096, 256, 32), (4096, 256, 256), (1000, 40, 17), (5, 3, 2),
+                                   (70000, 8, 8)])
+def test_gram_matches_fp64(env, m, p, q):
+    """A^T B of tall float64 panels (the Krylov block's Gram and cross products)."""
+    torch, dev = env
+    from admmq import panel
+    g = torch.Generator(device="cpu").manual_seed(m + p + q)
+    A = torch.randn(m, p, generator=g, dtype=torch.float64).to(dev)
+    B = torch.randn(m, q, generator=g, dtype=torch.float64).to(dev)
+    C = panel.gram(A, B)
+    assert C.shape == (p, q)
+    assert _colrel(C, A.T @ B) < 1e-13
+    assert torch.equal(C, panel.gram(A, B))
+    Ct = panel.gram(A.T.contiguous().T, B)   # a column-major A (copied to rows)
+    assert torch.equal(C, Ct)
 
 
 def test_panel_argument_errors(env):

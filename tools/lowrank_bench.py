@@ -116,7 +116,8 @@ def main():
            "krylov_blocks_mean": sum(kry.blocks) / len(kry.blocks), "krylov_residual_max": max(kry.residuals),
            "rel_history": hist, "reference_rel_history_real_weights": [32.1919, 1.0278, 1.0150, 1.0079],
            "projection_checks": checks,
-           "max_rel_vs_exact_f64": max(c["rel_vs_exact_f64"] for c in checks),
+           "max_rel_vs_exact_f64": max((c["rel_vs_exact_f64"] for c in checks), default=float("nan")),
+           "krylov_orthogonality_repairs": kry.repairs,
            "exact_svd_projection_s": svd_s,
            "exact_svd_loop_estimate_s": {"reference_schedule_max": svd_s * sched_max, "this_loop_schedule": svd_s * nr,
                                          "reference_schedule_max_projections": sched_max, "this_loop_projections": nr}}

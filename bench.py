@@ -136,13 +136,16 @@ def run_step(work, max_iter_admm, num_attempts=200):
     return runs
 
 
+USE_DIST = False   # torch.distributed (RCCL) on: world > 1, or --force-dist (exercises the collectives at N = 1)
+
+
 def gather_factors(runs, rank, world, numel, device):
     """The single collective of the path: every rank's converged factors to rank 0 (one
     RCCL gather over xGMI). Sizes are static (numel from the shard plan), so the flat
     buffers are padded to the largest rank's size and no size exchange is needed."""
     flat = torch.cat([f.reshape(-1) for r in runs for f in r.factors]) if runs else torch.zeros(0, device=device)
     assert flat.numel() == numel[rank], (flat.numel(), numel[rank])
-    if world == 1:
+    if world == 1 and not USE_DIST:
         return flat.numel()
     buf = torch.zeros(max(numel), device=device)
     buf[:flat.numel()] = flat
@@ -156,7 +159,7 @@ def reduce_over_ranks(elapsed, factor_iters, world, device):
     factor-iterations all ranks processed (SUM)."""
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     fi = torch.tensor([float(factor_iters)], device=device, dtype=torch.float64)
-    if world > 1:
+    if world > 1 or USE_DIST:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(fi, op=dist.ReduceOp.SUM)
     return float(el.item()), float(fi.item())
@@ -284,20 +287,26 @@ def step_roofline(work, max_iter_admm, ms_per_step, num_attempts=200):
             "split_solve_note": "solve term at the split form's f16 MFMA peak / 3 products (838.9 TF/s)"}
 
 
-TRAFFIC_TAG = "r03"
+TRAFFIC_TAGS = ("r04", "r03")   # newest first
 
 
 def load_traffic(model, split):
     """Per-launch HBM bytes of each launch class from the committed rocprofv3 PMC passes of
-    THIS config (profiles/<tag>_<model>_traffic.json, tools/traffic_json.py); PMC counters
-    cannot be read live inside the timed region. None when no file matches the config."""
-    path = os.path.join(ROOT, "profiles", f"{TRAFFIC_TAG}_{model}_traffic.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if t.get("split", True) != split:
+    THIS config (profiles/<tag>_<model>_traffic.json, tools/traffic_json.py; the newest
+    round that profiled it); PMC counters cannot be read live inside the timed region. None
+    when no file matches the config."""
+    t = None
+    for tag in TRAFFIC_TAGS:
+        path = os.path.join(ROOT, "profiles", f"{tag}_{model}_traffic.json")
+        try:
+            with open(path) as f:
+                cand = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if cand.get("split", True) == split:
+            t = cand
+            break
+    if t is None:
         return None
     t["file"] = os.path.relpath(path, ROOT)
     return t
@@ -469,6 +478,9 @@ def main():
                          "the launch's CU-level LPT makespan (a parallel piece priced COST K-steps extra); same bits")
     ap.add_argument("--gemm-stage", type=int, default=-1,
                     help="A/B: fp32 64x64 staging form 0..4 (library default 3; 2 = 2-deep ring, 4 tiles per CU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed (RCCL) and run the gather / all-reduce even at N = 1 "
+                         "(launch under torch.distributed.run): exercises the multi-GPU path on one GPU")
     ap.add_argument("--fin-nv3", type=int, default=1, choices=[0, 1],
                     help="A/B: 1 (library default) = three float4 groups per search thread where that keeps the "
                          "finalize in the search launch (C4), 0 = at most two (separate finalize launch at C4)")
@@ -484,7 +496,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    global USE_DIST
+    USE_DIST = world > 1 or a.force_dist
+    if USE_DIST:
         dist.init_process_group("nccl", device_id=device)
 
     from admmq import _lib
@@ -514,7 +528,7 @@ def main():
     if prof:
         n_launch = a.steps * 3 * 6 * (a.max_iter_admm // a.prof_every + 1) + 64
         _lib.check(lib.admmq_profile_begin(n_launch, a.prof_every), "profile_begin")
-    if world > 1:
+    if USE_DIST:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -522,7 +536,7 @@ def main():
         runs = run_step(work, a.max_iter_admm)
         gather_factors(runs, rank, world, numel, device)
     torch.cuda.synchronize()
-    if world > 1:
+    if USE_DIST:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern = None
@@ -592,7 +606,7 @@ def main():
             except Exception as e:  # parity is reported, never blocks the perf line
                 out["parity_error"] = repr(e)[:200]
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if USE_DIST:
         dist.destroy_process_group()
 
 

@@ -367,18 +367,21 @@ __global__ __launch_bounds__(256) void k_gram64(const double* __restrict__ A, in
       }
 }
 
-// one wave per tile: the S partials in order, then the D map (row (lane >> 4) + 4 v of the
-// p-tile a, column lane & 15 of the q-tile u)
-__global__ __launch_bounds__(64) void k_gram64_sum(const double* __restrict__ part, int S, int p, int q,
-                                                   double* __restrict__ C, int ldc) {
-  const int lane = threadIdx.x;
+// the S partials of a tile in slice order: thread v of 256 sums values v, v + 256, ... of the
+// tile's 1024 (x = value / 64, lane = value % 64), loads issued 8 slices ahead; then the D
+// map (row (lane >> 4) + 4 v of the p-tile a, column lane & 15 of the q-tile u)
+__global__ __launch_bounds__(256) void k_gram64_sum(const double* __restrict__ part, int S, int p, int q,
+                                                    double* __restrict__ C, int ldc) {
   const int tq = (q + 31) / 32;
   const int p0 = (blockIdx.x / tq) * 32, q0 = (blockIdx.x % tq) * 32;
   const double* src = part + (size_t)blockIdx.x * S * 16 * 64;
 #pragma unroll
-  for (int x = 0; x < 16; ++x) {
-    double sum = src[x * 64 + lane];
-    for (int g = 1; g < S; ++g) sum += src[((size_t)g * 16 + x) * 64 + lane];
+  for (int k = 0; k < 4; ++k) {
+    const int val = threadIdx.x + 256 * k;
+    double sum = src[val];
+#pragma unroll 8
+    for (int g = 1; g < S; ++g) sum += src[(size_t)g * 1024 + val];
+    const int x = val >> 6, lane = val & 63;
     const int a = x >> 3, u = (x >> 2) & 1, v = x & 3;
     const int r = p0 + 16 * a + (lane >> 4) + 4 * v, c = q0 + 16 * u + (lane & 15);
     if (r < p && c < q) C[(size_t)r * ldc + c] = sum;
@@ -467,7 +470,7 @@ int32_t admmq_gram64(const double* A, int64_t lda, const double* B, int64_t ldb,
   hipStream_t s = static_cast<hipStream_t>(stream);
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(k_gram64, dim3(tiles, S), dim3(256), 0, s, A, (int)lda, B, (int)ldb, (int)m, (int)p, (int)q, part);
-  hipLaunchKernelGGL(k_gram64_sum, dim3(tiles), dim3(64), 0, s, part, S, (int)p, (int)q, C, (int)q);
+  hipLaunchKernelGGL(k_gram64_sum, dim3(tiles), dim3(256), 0, s, part, S, (int)p, (int)q, C, (int)q);
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "gram64: launch failed");
 }
 

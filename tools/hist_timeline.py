@@ -56,7 +56,7 @@ if fused:   # fused finalize: column 4 = selection received, 5 = finalize done
     print(f"  fused finalize: span to last finalize {(t1 - t0) / 100:.2f} us")
 for name, j0, j1 in phases:
     d = [(r[j1] - r[j0]) / 100 for r in rows]
-    print(f"  {name:13s} avg {sum(d)/len(d):7.2f}  max {max(d):7.2f} us")
+    print(f"  {name:13s} avg {sum(d)/len(d):7.2f}  max {max(d):7.2f}  min {min(d):7.2f} us")
 starts = sorted((r[0] - t0) / 100 for r in rows)
 print("  start offsets: median %.2f  90%% %.2f  max %.2f us" % (starts[len(starts) // 2], starts[int(0.9 * len(starts))], starts[-1]))
 if fused and hasattr(lib, "admmq_debug_fin_trace"):

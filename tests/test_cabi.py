@@ -144,3 +144,25 @@ def test_ksplit_pieces_by_shape(lib):
     for (I, R), n in expect.items():
         assert lib.admmq_debug_ksplit_pieces(I, R) == n, (I, R, lib.admmq_debug_ksplit_pieces(I, R))
     assert lib.admmq_debug_ksplit_pieces(0, 5) == 0
+
+
+def test_panel_entry_points_check_arguments(lib):
+    """The rank projection's panel products (admmq_panel_*, admmq_gram64): workspace sizes
+    and argument / workspace checks answered on the host before any launch."""
+    P = ctypes.c_void_p
+    one = P(16)   # a non-null dummy address: every call below is refused before a launch
+    assert lib.admmq_panel_workspace_size(4096, 4096, 32) >= 64 * 4 * 64 * 32 * 8
+    assert lib.admmq_panel_workspace_size(0, 4096, 32) == 0
+    big = lib.admmq_panel_workspace_size(4096, 4096, 256)
+    assert big > lib.admmq_panel_workspace_size(4096, 4096, 32)
+    ERR_ARG, ERR_WS = -1, -3
+    assert lib.admmq_panel_xtq(None, 8, 8, 8, one, 4, one, one, 1 << 20, None) == ERR_ARG
+    assert lib.admmq_panel_xtq(one, 8, 8, 7, one, 4, one, one, 1 << 20, None) == ERR_ARG      # ldx < n
+    assert lib.admmq_panel_xy(one, 8, 8, 8, one, 4, one, one, 16, None) == ERR_WS            # workspace too small
+    assert lib.admmq_panel_xy(one, 8, 8, 8, one, 4, one, None, 1 << 20, None) == ERR_WS
+    assert lib.admmq_panel_outer(one, one, 8, 8, 33, one, 8, None) == ERR_ARG                # rank above 32
+    assert lib.admmq_panel_outer(one, one, 8, 8, 4, one, 7, None) == ERR_ARG                 # ldo < n
+    assert lib.admmq_gram64_workspace_size(4096, 32, 32) >= 16 * 16 * 64 * 8
+    assert lib.admmq_gram64(one, 3, one, 4, 8, 4, 4, one, one, 1 << 20, None) == ERR_ARG     # lda < p
+    assert lib.admmq_gram64(one, 4, one, 4, 8, 4, 4, one, one, 8, None) == ERR_WS
+    assert b"workspace" in lib.admmq_last_error()

@@ -107,3 +107,15 @@ def gram(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -
     _lib.check(lib.admmq_gram64(_lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), m, p, q, _lib.ptr(C), _lib.ptr(ws),
                                 ws.numel(), _lib.stream_handle(A.device)), "gram64")
     return C
+
+
+def epc_mu(c: torch.Tensor, s: torch.Tensor, normY2: float, delta2: float) -> torch.Tensor:
+    """The EPC multiplier (``admmq.parafac_epc._solve_mu``) on the device: a 0-dim float64
+    tensor, with no host synchronisation."""
+    if c.dtype != torch.float64 or s.dtype != torch.float64 or c.shape != s.shape or c.dim() != 1:
+        raise ValueError("admmq.panel.epc_mu: c and s must be float64 vectors of one length")
+    c, s = c.contiguous(), s.contiguous()
+    mu = torch.empty((), dtype=torch.float64, device=c.device)
+    _lib.check(_lib.load().admmq_epc_mu(_lib.ptr(c), _lib.ptr(s), c.numel(), float(normY2), float(delta2), _lib.ptr(mu),
+                                        _lib.stream_handle(c.device)), "epc_mu")
+    return mu

@@ -22,17 +22,19 @@ runs on the fp64 HIP kernels (``als.gram_mttkrp_f64`` -> ``csrc/cp64_kernels.hip
 MFMA with the Khatri-Rao operand formed on the fly); the reconstruction errors use the
 CP identity ||Y||^2 - 2 <Y, [[w; U]]> + ||[[w; U]]||^2 on those products (no I x J x K
 reconstruction, as tensorly's ``parafac`` does); the R x R solves / eigendecompositions
-are torch linear algebra on the device, the scalar root search for mu runs on the host.
+are torch linear algebra on the device, and the EPC step's scalar root search for mu runs
+on the device as well (``panel.epc_mu``, ``csrc/epc_kernels.hip``: no host synchronisation
+per mode step).
 Float64 tensors on the GPU only: a CPU tensor raises (no CPU path).
 """
 from __future__ import annotations
 
 from typing import List, Optional, Sequence, Tuple
 
-import numpy as np
 import torch
 
 from .als import gram_mttkrp_f64
+from .panel import epc_mu
 
 
 def _khatri_rao(mats: List[torch.Tensor]) -> torch.Tensor:
@@ -96,27 +98,6 @@ def parafac(tensor: torch.Tensor, rank: int, init: str = "random", random_state=
     return weights, fs
 
 
-def _solve_mu(c: np.ndarray, s: np.ndarray, normY2: float, delta2: float) -> float:
-    """Root mu >= 0 of normY2 - sum c (s + 2 mu) / (s + mu)^2 = delta2 (increasing in mu)."""
-    def err(mu: float) -> float:
-        return normY2 - float(np.sum(c * (s + 2 * mu) / (s + mu) ** 2))
-    if err(0.0) >= delta2:
-        return 0.0
-    hi = max(float(s.max()), 1e-300)
-    while err(hi) < delta2 and hi < 1e300:
-        hi *= 2.0
-    lo = 0.0
-    for _ in range(200):   # bisection to fp64 resolution of the bracket
-        mid = 0.5 * (lo + hi)
-        if mid <= lo or mid >= hi:
-            break
-        if err(mid) < delta2:
-            lo = mid
-        else:
-            hi = mid
-    return lo   # the feasible end of the bracket: err(lo) < delta2
-
-
 def cp_anc(tensor: torch.Tensor, rank: int, delta: float, weights: Optional[torch.Tensor] = None,
            factors: Optional[Sequence[torch.Tensor]] = None, maxiter: int = 5000, tol: float = 1e-5
            ) -> Tuple[torch.Tensor, List[torch.Tensor]]:
@@ -142,7 +123,7 @@ def cp_anc(tensor: torch.Tensor, rank: int, delta: float, weights: Optional[torc
             s, V = torch.linalg.eigh(G)
             s = s.clamp_min(0.0)
             Ft = F @ V
-            mu = _solve_mu(torch.sum(Ft * Ft, dim=0).cpu().numpy(), s.cpu().numpy(), normY2, delta2)
+            mu = epc_mu(torch.sum(Ft * Ft, dim=0), s, normY2, delta2)   # on the device: no host sync
             fs[m] = (Ft / (s + mu).clamp_min(1e-300)) @ V.T
         lam = torch.linalg.norm(fs[n - 1], dim=0)
         lnorm = float(torch.linalg.norm(lam))

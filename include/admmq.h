@@ -281,6 +281,12 @@ size_t admmq_gram64_workspace_size(int64_t m, int64_t p, int64_t q);
 int32_t admmq_gram64(const double* A, int64_t lda, const double* B, int64_t ldb, int64_t m, int64_t p, int64_t q,
                      double* C, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The EPC step's multiplier (cp_anc, source/parafac_epc.py:61-74): *mu (device double) = the
+ * root mu >= 0 of normY2 - sum_i c_i (s_i + 2 mu) / (s_i + mu)^2 = delta2 (0 when already
+ * below), by bracket doubling and bisection to fp64 resolution; c, s: n device doubles. */
+int32_t admmq_epc_mu(const double* c, const double* s, int64_t n, double normY2, double delta2, double* mu,
+                     void* stream);
+
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);
 const char* admmq_last_error(void);

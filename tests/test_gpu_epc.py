@@ -97,3 +97,21 @@ def test_parafac_epc_resnet18_layer_timing():
     epc_err = float((W - eo._reconstruct(lam, Us)).norm() / W.norm())
     print(f"parafac-epc layer1.0.conv1 R={R}: {t:.2f} s, ALS rel err {als_err:.4f}, EPC rel err {epc_err:.4f}")
     assert np.isfinite(epc_err) and epc_err <= als_err * (1 + 1e-6)
+
+
+@pytest.mark.parametrize("R,seed", [(134, 1), (13, 2), (1141, 3), (5, 4)])
+def test_epc_mu_device_matches_oracle(R, seed):
+    """The EPC multiplier solved on the device (admmq_epc_mu: bracket doubling + bisection to
+    fp64 resolution, one workgroup) against the oracle's host restatement of the same root
+    search: within a few ulps of the bracket (the sum over the R terms runs in another
+    order); 0 when the unconstrained step already meets delta."""
+    from admmq import panel
+    g = torch.Generator().manual_seed(seed)
+    s = torch.rand(R, generator=g, dtype=torch.float64) * 10.0
+    s[0] = 0.0   # a zero eigenvalue (clamped) as cp_anc can see
+    c = torch.rand(R, generator=g, dtype=torch.float64)
+    normY2 = float(torch.sum(c / s.clamp_min(1e-3))) * 2.0
+    for delta2 in (normY2 * 0.5, normY2 * 0.999, normY2 * 2.0):
+        ref = eo._solve_mu(c, s, normY2, delta2)
+        got = float(panel.epc_mu(c.cuda(), s.cuda(), normY2, delta2))
+        assert abs(got - ref) <= 1e-12 * max(abs(ref), 1e-300) or (ref == 0.0 and got == 0.0), (delta2, got, ref)

@@ -416,12 +416,17 @@ def emulate_shards(a):
     _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
     _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
     _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
+    if a.gemm_stage >= 0:
+        _lib.check(lib.admmq_debug_set_gemm_stage(a.gemm_stage), "gemm_stage")
     N = a.emulate_world
-    full, _, _ = build_workload(a.model, 0, 1, "layers", device)
-    full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
-    del full
+    only = [int(v) for v in a.emulate_only.split(",")] if a.emulate_only else None
+    full_ms = None
+    if only is None:
+        full, _, _ = build_workload(a.model, 0, 1, "layers", device)
+        full_ms = time_steps(full, a.max_iter_admm, a.steps, a.warmup)
+        del full
     shard_ms, nlayers, info, shard_us, shard_cost = [], [], None, [], []
-    for r in range(N):
+    for r in (only if only is not None else range(N)):
         work, _, info = build_workload(a.model, r, N, "layers", device)
         shard_cost.append(sum(layer_cost(s, R) for (s, _, R, _) in work))
         nlayers.append(len(work))
@@ -434,7 +439,8 @@ def emulate_shards(a):
            "shard_ms_per_sweep": shard_ms, "layers_per_rank": nlayers, "busiest_ms": max(shard_ms),
            "shard_cost": shard_cost, "total_cost": sum(layer_cost(s, s.rank()) for s in _model_specs(a.model)),
            "shard_kernel_avg_us": shard_us,
-           "implied_speedup": full_ms / max(shard_ms), "lpt_speedup_cap": info["lpt_speedup_cap"],
+           "ranks": only if only is not None else list(range(N)),
+           "implied_speedup": full_ms / max(shard_ms) if full_ms else None, "lpt_speedup_cap": info["lpt_speedup_cap"],
            "whole_layer_speedup_cap": info["whole_layer_speedup_cap"], "policy": info["policy"]}
     print(json.dumps(out), flush=True)
 
@@ -470,6 +476,8 @@ def main():
     ap.add_argument("--ksplit", type=int, default=1, choices=[0, 1],
                     help="A/B: K-split of the fp32 solve tiles of factors too small to fill the chip (1, default: "
                          "pieces fixed by each factor's shape) or never (0)")
+    ap.add_argument("--emulate-only", default="",
+                    help="with --emulate-world: time only these ranks' shards (comma list), not the whole model")
     ap.add_argument("--ksplit-form", type=int, default=1, choices=[0, 1, 2],
                     help="A/B: K-split pieces run in parallel where the launch leaves CUs idle (1, default), always "
                          "serially in one workgroup (0) or always in parallel (2); same bits")

@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--shapes", default="", help="I:R,I:R,... instead of the resnet18 factors of --mode")
+ap.add_argument("--ksplit-form", type=int, default=1)
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 g = torch.Generator().manual_seed(0)
@@ -34,6 +35,7 @@ for I, R in shapes:
     H = torch.randn(I, R, generator=g).to(dev) * 0.1
     U = torch.zeros(I, R, device=dev)
     probs.append((H, U, F, G))
+_lib.check(_lib.load().admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
 admm_iteration_batched(probs, a.iters, 0.0, 4, "tensor_mseminmax_symmetric", check_spd=False)
 torch.cuda.synchronize()
 lib = _lib.load()
@@ -47,8 +49,8 @@ for b in range(got):
     t0, t1, hid = buf[4 * b], buf[4 * b + 1], buf[4 * b + 2]
     if t1 > t0:
         clk.append(buf[4 * b + 3] / ((t1 - t0) / 100.0) / 1e3)   # shader cycles per us -> GHz
-    if t0 == 0 or t1 < t0:
-        break
+    if t0 == 0 or t1 < t0:   # grid padding (empty tiles leave no record)
+        continue
     wg = (hid >> 48) & 0x7FFF
     nk = (hid >> 40) & 0xFF
     xcc = (hid >> 32) & 0xFF
@@ -93,7 +95,7 @@ cnt = collections.Counter(len(v) for v in per_cu.values())
 print("workgroups per CU histogram:", dict(sorted(cnt.items())), "CUs", len(per_cu))
 # placement check for the CU-balanced tile order: do workgroups b and b + 256 share a CU?
 where = {r[7]: (r[3], r[4], r[5], r[6]) for r in recs}
-pairs = [(b, b + 256) for b in range(len(recs)) if b + 256 in where and b in where]
+pairs = [(b, b + 256) for b in range(max(where) + 1) if b + 256 in where and b in where]
 same = sum(1 for a, b in pairs if where[a] == where[b])
 print(f"placement: workgroups b and b+256 on the same CU for {same}/{len(pairs)} pairs; "
       f"same XCD for {sum(1 for a, b in pairs if where[a][0] == where[b][0])}/{len(pairs)}")

@@ -57,7 +57,8 @@ struct MseView {
   double* s2;                  // [slot]
   int* sel;                    // [slot][2 + kMaxSel]
   unsigned* ticket;            // [slot] stage-1 blocks finished (the last one runs the selection)
-  unsigned* ready;             // [slot] fused finalize: iteration + 1 once the selection is published
+  unsigned long long* ready;   // [slot] fused finalize: (iteration + 1) << 32 once the selection is published,
+                               // | 1 << 31 | c* when the selection is the single candidate c*
   const int* done;             // early-exit flag (ADMM) or nullptr
   int nhist, pad_;             // stage-1 blocks of this job
 };

@@ -414,7 +414,7 @@ static void carve_view(Carver& cv, MseView& v, int nslot, int ncand) {
   v.s2 = cv.take<double>((size_t)nslot);
   v.sel = cv.take<int>((size_t)nslot * (2 + kMaxSel));
   v.ticket = cv.take<unsigned>((size_t)nslot);
-  v.ready = cv.take<unsigned>((size_t)nslot);
+  v.ready = cv.take<unsigned long long>((size_t)nslot);
 
 }
 
@@ -453,7 +453,7 @@ struct AdmmPlan {
   int* d_small = nullptr;
   int nfin_big = 0, nhist_big = 0;   // finalize / stage-1 units of the other jobs (listed first)
   bool rows_aligned = true;          // every big job's stage-1 units are whole rows (fused finalize possible)
-  unsigned* d_ready = nullptr;       // [nprob][2] fused-finalize ready words (zeroed per run)
+  unsigned long long* d_ready = nullptr;   // [nprob][2] fused-finalize ready words (zeroed per run)
   unsigned* d_kctr = nullptr;        // K-split arrival counters (zeroed per run)
   size_t nkctr = 0;
   bool ksplit_par = false;           // this launch runs the K-split pieces in parallel (else serially)
@@ -996,7 +996,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
   long long small_max = 0;
   for (int i : pl.small) small_max = std::max(small_max, (long long)pl.desc[i].I * pl.desc[i].ld);
   pl.small_groups = small_admm_groups(small_max);
-  pl.d_ready = cv.take<unsigned>(2 * (size_t)nprob);
+  pl.d_ready = cv.take<unsigned long long>(2 * (size_t)nprob);
   for (int i = 0; i < nprob; ++i) pl.desc[i].mv.ready = pl.d_ready ? pl.d_ready + 2 * i : nullptr;
   pl.d_desc = cv.take<ProbDesc>(nprob);
   pl.d_tiles = cv.take<GemmTile>(pl.tiles.size());
@@ -1512,7 +1512,7 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   const int nfin_blocks = nh_big;
   const bool fuse_fin = fin_ok && fin_cap > 0 && nfin_blocks <= fin_cap;
   const unsigned polls = g_fin_wait_polls.load();
-  if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned), s) != hipSuccess)
+  if (fuse_fin && hipMemsetAsync(pl.d_ready, 0, 2 * (size_t)nprob * sizeof(unsigned long long), s) != hipSuccess)
     return check_hip("ready reset");
   // every problem thin: all iterations in one persistent launch (k_thin_loop) when the
   // fused paths are allowed (the op's fault retry turns them off) and it fits the device

@@ -1075,14 +1075,25 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     }
     sse_in_block(v, lsel, n, QMAX == 1 ? 1 : 31 - __builtin_clz(QMAX) + 1, slot, mx, reinterpret_cast<float4*>(smem));
     trace(ADMMQ_NOW());
-    if constexpr (FIN) {   // publish: the record write-through, drained, then the ready word
-      const int nrec = 2 + min(lsel[0], kMaxSel);
-      for (int j = threadIdx.x; j < nrec; j += blockDim.x)
-        __hip_atomic_store(sel + j, lsel[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0)
-        __hip_atomic_store(v.ready + slot, (unsigned)(iter + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (FIN) {
+      // publish. A single candidate c* (nearly always) travels in the ready word itself,
+      // (iter + 1) << 32 | 1 << 31 | c*: the waiting blocks need nothing else, so neither the
+      // record's write-through stores nor their drain sit before it (the record keeps the
+      // plain stores of select_block for the later launches). Otherwise the record
+      // write-through, drained, then the ready word.
+      const unsigned long long tag = (unsigned long long)(unsigned)(iter + 1) << 32;
+      if (lsel[0] == 1) {
+        if (threadIdx.x == 0)
+          __hip_atomic_store(v.ready + slot, tag | 0x80000000ull | (unsigned)lsel[2], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const int nrec = 2 + min(lsel[0], kMaxSel);
+        for (int j = threadIdx.x; j < nrec; j += blockDim.x)
+          __hip_atomic_store(sel + j, lsel[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(v.ready + slot, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   } else {
     trace(T3);
@@ -1094,7 +1105,9 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
       if (threadIdx.x == 0) {
         unsigned polls = 0;
         int to = 0;
-        while (__hip_atomic_load(v.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)(iter + 1)) {
+        unsigned long long w;
+        while (((w = __hip_atomic_load(v.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+               (unsigned long long)(unsigned)(iter + 1)) {
           __builtin_amdgcn_s_sleep(2);
           if (++polls >= wait_polls) {
             __hip_atomic_store(p.flags + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1103,8 +1116,13 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
           }
         }
         timed_out = to;
-        lsel[0] = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lsel[2] = __hip_atomic_load(sel + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!to && (w & 0x80000000ull)) {   // the single candidate, from the ready word
+          lsel[0] = 1;
+          lsel[2] = (int)(w & 0x7FFFFFFFull);
+        } else {
+          lsel[0] = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lsel[2] = __hip_atomic_load(sel + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       __syncthreads();
       if (timed_out) {   // internal fault: leave the elements unfinalized (the caller re-runs)

@@ -136,14 +136,16 @@ struct ThinLoopUnit { int job, col0, cw, rank, nteam, pad_[3]; };
 constexpr int kTLThreads = 512;
 constexpr int kTLMaxCand = 256;       // num_attempts of the persistent loop
 constexpr int kTLBins = 264;          // >= kTLMaxCand + 1, a whole number of 64-B lines
+constexpr int kTLMaxTeam = 64;        // workgroups of a team (ld / 32 <= 36; one polling wave)
 constexpr int kTLKPairs = 9;          // k pairs of M per thread and reduction chunk (ld <= 1152 per chunk)
 // A team's hand-off words, one set per parity slot (zeroed by the host before the launch;
 // after that rank 0 re-zeroes a slot once every reader is past it). 128-B lines apart.
 struct alignas(128) ThinSync {
   unsigned bar;                          // barrier arrivals (monotonic)
   unsigned pad0_[31];
-  unsigned long long mx[2];              // max |X| bits per slot
+  unsigned long long mx[2];              // (unused since the barrier-1 words carry max |X|)
   unsigned long long pad1_[14];
+  unsigned long long arr1[kTLMaxTeam];   // barrier 1: per team rank, (iteration + 1) << 32 | its max |X| bits
   double s2[2];                          // sum X^2 per slot (stage-1 bound)
   double res[2][4];                      // residual sums S1..S4 per slot
   double pad2_[6];

@@ -549,17 +549,36 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
     amax = wave_max_u32(amax);
     if (lane == 0) s_amax[wave] = amax;
     __syncthreads();
+    // ---- barrier 1: the team's max |X|. The arrival IS the hand-off: each workgroup
+    // stores (it + 1) << 32 | its max into its own word (agent scope, one lane); wave 0
+    // polls the team's words, lane l word l, until every tag is this iteration's, and
+    // takes their max - no counter, no drain of other stores (nothing else is handed over
+    // here), no second load after the wait. The words are zeroed by the host per launch
+    // and tagged per iteration, so they are never reset.
+    const unsigned long long tag = (unsigned long long)(unsigned)(it + 1) << 32;
     if (tid == 0) {
       unsigned mm = 0u;
 #pragma unroll
       for (int w = 0; w < kTLThreads / 64; ++w) mm = max(mm, s_amax[w]);
-      if (mm) atomicMax(&sy.mx[slot], (unsigned long long)mm);
+      ast_u64(&sy.arr1[un.rank], tag | mm);
     }
-    // ---- barrier 1: the team's max |X|
     ADMMQ_TL_PH(2);
-    if (!team_barrier(&sy.bar, nteam * ++nbar, wait_polls, &s_ok)) { fault = true; break; }
-    if (tid == 0) s_mx = ald_u64(&sy.mx[slot]);
+    if (wave == 0) {
+      unsigned long long w = tag;
+      int ok = 1;
+      if (lane < nteam) {
+        unsigned n = 0;
+        while (((w = ald_u64(&sy.arr1[lane])) & ~0xFFFFFFFFull) != tag) {
+          if (++n > wait_polls) { ok = 0; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      const unsigned m = wave_max_u32((unsigned)w);
+      const bool all_ok = __ballot(!ok) == 0ull;
+      if (lane == 0) { s_mx = m; s_ok = all_ok ? 1 : 0; }
+    }
     __syncthreads();
+    if (!s_ok) { fault = true; break; }
     ADMMQ_TL_PH(3);
     const float mx = __uint_as_float((unsigned)s_mx);
     QParams qp;
@@ -789,7 +808,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
         ast_u64(&sy.h2[slot][b], 0ull);
         ast_u64(&sy.sse[slot][b], 0ull);
       }
-      if (tid == 0) { ast_u64(&sy.mx[slot], 0ull); ast_f64(&sy.s2[slot], 0.0); }
+      if (tid == 0) ast_f64(&sy.s2[slot], 0.0);
       if (tid < 4) ast_f64(&sy.res[slot ^ 1][tid], 0.0);
     }
     ADMMQ_TL_PH(13);
@@ -807,6 +826,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   }
 }
 
+static_assert(1152 / 32 <= kTLMaxTeam, "a team of ld / 32 workgroups polls in one wave");
 int launch_thin_loop(const ProbDesc* d, const ThinLoopUnit* units, int nunits, ThinSync* sync, int nr, int maxld,
                      int n_iter, float eps, int ncand, int bits, unsigned wait_polls, int ncu, hipStream_t s) {
   if (nunits <= 0 || nunits > ncu || n_iter <= 0 || maxld > 1152) return -1;

@@ -122,6 +122,7 @@ def load() -> ctypes.CDLL:
         "admmq_quantize_channel_workspace_size": (S, [P, I32, I32]),
         "admmq_quantize_channel": (I32, [P, P, P, I32, I32, I32, I32, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
+        "admmq_debug_set_sel_widen": (I32, [I32]),
         "admmq_set_solve_mode": (I32, [I32]),
         "admmq_get_solve_mode": (I32, []),
         "admmq_debug_set_legacy_stage1": (I32, [I32]),
@@ -235,6 +236,21 @@ class exhaustive_search:
 
     def __exit__(self, *exc):
         load().admmq_set_exhaustive_search(0)
+        return False
+
+
+class sel_widen:
+    """Context manager (diagnostics): keep every candidate in the two-stage search's
+    selected set, so its multi-candidate paths - the canonical SSEs, and in the fused
+    finalize the record published before the ready word, and the thin loop's stage 2 - run
+    on every call. The answer is exact either way, so the bits are the same."""
+
+    def __enter__(self):
+        check(load().admmq_debug_set_sel_widen(1), "sel_widen")
+        return self
+
+    def __exit__(self, *exc):
+        check(load().admmq_debug_set_sel_widen(0), "sel_widen")
         return False
 
 

@@ -227,6 +227,8 @@ void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int 
                  bool split, int slot, int iter, float eps, int ncand, hipStream_t s, hipEvent_t ev0 = nullptr,
                  hipEvent_t ev1 = nullptr, bool prefetch_u = false);
 extern int g_gemm_ks_f32;
+int set_sel_widen_search(int on);   // diagnostics (mse_search.hip / thin_loop.hip)
+int set_sel_widen_thin(int on);
 extern int g_gemm_f32_stage;   // fp32 64 x 64 staging form (gemm_kernels.hip)
 void launch_gemm_f32t(const ProbDesc* d, const GemmTile* tiles, int ntiles, int slot, int iter, float eps, int ncand,
                       hipStream_t s);

@@ -1335,6 +1335,13 @@ int64_t admmq_debug_ksplit_balance_count(const int32_t* IR, int32_t nprob) {
   }
   return ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
 }
+// diagnostics: keep every candidate in the selected set S (1) or the rigorous set (0, default):
+// the multi-candidate paths run every time, with the same exact answer
+int32_t admmq_debug_set_sel_widen(int32_t on) {
+  if (on < 0 || on > 1) return fail(ADMMQ_ERR_ARG, "sel widen must be 0 or 1");
+  if (set_sel_widen_search(on) != 0 || set_sel_widen_thin(on) != 0) return check_hip("sel widen");
+  return ADMMQ_OK;
+}
 // diagnostics: the K-split pieces the planner gives an (I, R) factor (0 on bad arguments)
 int32_t admmq_debug_ksplit_pieces(int32_t I, int32_t R) {
   if (I <= 0 || R <= 0) return 0;

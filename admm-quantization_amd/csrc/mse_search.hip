@@ -83,6 +83,13 @@ int copy_hist_trace(unsigned long long* host, int n) {
 // 2..kMaxSel, exhaustive} counts since the last reset), for admmq_debug_sel_stats.
 __device__ unsigned long long g_sel_stats[3];
 __device__ int g_no_stop = 0;   // stop flag of units without one (standalone quantization)
+// Diagnostics (admmq_debug_set_sel_widen): every candidate stays in S, so the selection's
+// multi-candidate paths (the canonical SSEs; in the fused finalize the record published
+// before the ready word) run every time; the exact answer, hence every bit, is the same.
+__device__ int g_sel_widen = 0;
+int set_sel_widen_search(int on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sel_widen), &on, sizeof(int)) == hipSuccess ? 0 : -1;
+}
 int copy_sel_stats(unsigned long long* host, int reset) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sel_stats), sizeof(g_sel_stats)) != hipSuccess) return -1;
   if (reset) {
@@ -204,7 +211,7 @@ __device__ void select_wave(const MseView& v, int* sel, int* lsel, const unsigne
     for (int c = c1 - 1; c >= c0; --c) {
       double lo, hi;
       cx.bounds(c, t1, t2, lo, hi);
-      if (lo <= mymin) { keep |= 1ull << (c - c0); ++cnt; }
+      if (lo <= mymin || g_sel_widen != 0) { keep |= 1ull << (c - c0); ++cnt; }
       t1 += H1[c]; t2 += H2[c];
     }
   }
@@ -440,7 +447,7 @@ __device__ void select_wave2(const MseView& v, int* sel, int* lsel, const unsign
   for (int c = c0; c < c1; ++c) {
     double lo, hi;
     cx.bounds(c, T1v[c], T2v[c], lo, hi);
-    if (lo <= mymin) { keep |= 1ull << (c - c0); ++cnt; }
+    if (lo <= mymin || g_sel_widen != 0) { keep |= 1ull << (c - c0); ++cnt; }
   }
   int pre = cnt;                                   // inclusive prefix over lanes
 #pragma unroll
@@ -488,7 +495,7 @@ __device__ void select_block(const MseView& v, int* sel, int* lsel, unsigned lon
   __syncthreads();
   double mn = wmin[0];
   for (int k = 1; k < nw; ++k) mn = fmin(mn, wmin[k]);
-  const bool keep = c < n && lo <= mn;
+  const bool keep = c < n && (lo <= mn || g_sel_widen != 0);
   const unsigned long long bal = __ballot(keep);
   if (lane == 0) wcnt[w] = __popcll(bal);
   __syncthreads();

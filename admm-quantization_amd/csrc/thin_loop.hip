@@ -396,6 +396,12 @@ void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits,
 // X and max, barrier 1 + max load, threshold table, stage-1 inserts, stage-1 sums + flush,
 // barrier 2, team bins load, suffix sums + bounds + S, stage 2, finalize, barrier 3, slot
 // reset, stop test, iterations}
+// Diagnostics (admmq_debug_set_sel_widen): every candidate stays in S (stage 2 every
+// iteration; the same exact answer)
+__device__ int g_sel_widen_tl = 0;
+int set_sel_widen_thin(int on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sel_widen_tl), &on, sizeof(int)) == hipSuccess ? 0 : -1;
+}
 constexpr int kTLTraceMax = 1024;
 constexpr int kTLPhases = 16;
 __device__ unsigned long long g_tl_trace[kTLTraceMax][kTLPhases];
@@ -492,6 +498,7 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc(p.P, 0, (int)((size_t)p.Ip * ld * sizeof(float)), 0x00020000);
 
+  const bool widen = *(volatile int*)&g_sel_widen_tl != 0;
   unsigned nbar = 0;
   bool fault = false;
   unsigned long long ph[kTLPhases] = {}, tph = ADMMQ_NOW();
@@ -682,14 +689,14 @@ __global__ __launch_bounds__(kTLThreads) void k_thin_loop(const ProbDesc* __rest
         const double mn = wave_min_f64(hmin);
         unsigned cnt = 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (4 * lane + j < n && lo[j] <= mn) ? 1u : 0u;
+        for (int j = 0; j < 4; ++j) cnt += (4 * lane + j < n && (lo[j] <= mn || widen)) ? 1u : 0u;
         const unsigned suf = wave_suffix_u32(cnt);   // keeps in lanes >= this one
         const unsigned tot = __builtin_amdgcn_readfirstlane(suf);   // lane 0: all of them
         int pos = (int)(tot - suf);                  // keeps in lanes below this one
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int c = 4 * lane + j;
-          if (c < n && lo[j] <= mn) {
+          if (c < n && (lo[j] <= mn || widen)) {
             if (pos < kMaxSel) lsel[2 + pos] = c;
             ++pos;
           }

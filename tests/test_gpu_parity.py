@@ -137,6 +137,33 @@ def test_two_stage_admm_equals_exhaustive(torch_dev, stage1):
         assert _bits_equal(f[0], s_[0]) and _bits_equal(f[1], s_[1])
 
 
+def test_widened_selection_same_bits(torch_dev):
+    """The two-stage search's multi-candidate paths, forced (admmq.sel_widen: every
+    candidate stays in S, so the canonical SSEs decide): the fused finalize's record
+    published before the ready word (big factors), the thin loop's stage 2 (the all-thin
+    call) and the separate path give the bits of the default run, where S is nearly always
+    one candidate carried in the ready word (source/quantization.py:129-144 picks the same
+    candidate either way)."""
+    torch, dev = torch_dev
+    from admmq import admm_iteration_batched
+    from admmq._lib import sel_widen
+    big = [_layer_problem(l, m) for l, m in [("layer1.0.conv1", 0), ("layer2.0.conv2", 1), ("layer4.1.conv1", 0)]]
+    thin = [_layer_problem(l, 2) for l in ("layer1.0.conv1", "layer3.1.conv2")]
+
+    def run(probs, iters):
+        ps = [(_t(torch, dev, H), torch.zeros(H.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
+              for H, F, G in probs]
+        Hs = admm_iteration_batched(ps, iters, 0.0, 4, MSE)
+        return [(h.cpu().numpy(), p[1].cpu().numpy()) for h, p in zip(Hs, ps)]
+
+    for probs, iters in ((big, 4), (thin, 6)):
+        ref = run(probs, iters)
+        with sel_widen():
+            wide = run(probs, iters)
+        for a, b in zip(ref, wide):
+            assert _bits_equal(a[0], b[0]) and _bits_equal(a[1], b[1])
+
+
 def test_quantize_batched_equals_single(torch_dev):
     torch, dev = torch_dev
     from admmq import quantize_batched, quantize_tensor

@@ -123,6 +123,7 @@ def load() -> ctypes.CDLL:
         "admmq_quantize_channel": (I32, [P, P, P, I32, I32, I32, I32, P, S, P]),
         "admmq_set_exhaustive_search": (I32, [I32]),
         "admmq_debug_set_sel_widen": (I32, [I32]),
+        "admmq_debug_set_wide_min_tiles": (I32, [ctypes.c_int64]),
         "admmq_set_solve_mode": (I32, [I32]),
         "admmq_get_solve_mode": (I32, []),
         "admmq_debug_set_legacy_stage1": (I32, [I32]),

@@ -156,6 +156,9 @@ static constexpr int kF32Slots = 2;   // k_gemm_f32p workgroups per CU (72 KB of
 // (a lone layer4 conv: 144 tiles of 36 K-steps on 256 CUs, the busiest shard of a
 // multi-GPU run) splits every tile's K range into np pieces summed in piece order.
 static std::atomic<int> g_ksplit{1};
+// 64x64 tiles of a launch from which its I > 64 factors without a K-split take the 256x128
+// tiles (default kWideMinTiles; diagnostics: admmq_debug_set_wide_min_tiles; same bits)
+static std::atomic<long long> g_wide_min_tiles{kWideMinTiles};
 // execution form of the pieces (same bits either way): 1 = parallel only where the 64 x 64
 // launch's whole tiles leave CUs idle, else serial (default); 0 = always serial; 2 = always parallel
 static std::atomic<int> g_ksplit_par{1};
@@ -676,7 +679,7 @@ static int plan_admm(const admmq_problem* probs, int nprob, int ncand, void* ws,
     long long t64 = 0;
     for (int i = 0; i < nprob; ++i)
       if (probs[i].I > 32) t64 += (long long)((probs[i].I + 63) / 64) * ((rup(std::max(probs[i].R, 1), 32) + 63) / 64);
-    pl.wide = t64 >= kWideMinTiles;
+    pl.wide = t64 >= g_wide_min_tiles.load();
   }
   auto wide_prob = [&](const ProbDesc& d) { return pl.wide && d.I > 64 && d.ksplit == 1; };
   for (int i = 0; i < nprob; ++i)   // the split finalize needs whole rows in one unit
@@ -1334,6 +1337,12 @@ int64_t admmq_debug_ksplit_balance_count(const int32_t* IR, int32_t nprob) {
     }
   }
   return ksplit_balance(whole, cand, 256, f32_slots(), g_ksplit_cost.load());
+}
+// diagnostics: the wide-tile threshold (64x64 tiles per launch; default 4 x 768)
+int32_t admmq_debug_set_wide_min_tiles(int64_t t) {
+  if (t < 0) return fail(ADMMQ_ERR_ARG, "wide min tiles must be >= 0");
+  g_wide_min_tiles = t;
+  return ADMMQ_OK;
 }
 // diagnostics: keep every candidate in the selected set S (1) or the rigorous set (0, default):
 // the multi-candidate paths run every time, with the same exact answer

@@ -476,6 +476,8 @@ def main():
     ap.add_argument("--ksplit", type=int, default=1, choices=[0, 1],
                     help="A/B: K-split of the fp32 solve tiles of factors too small to fill the chip (1, default: "
                          "pieces fixed by each factor's shape) or never (0)")
+    ap.add_argument("--wide-min", type=int, default=-1,
+                    help="diagnostics: 64x64 tiles per launch from which factors take 256x128 tiles (default 3072)")
     ap.add_argument("--emulate-only", default="",
                     help="with --emulate-world: time only these ranks' shards (comma list), not the whole model")
     ap.add_argument("--ksplit-form", type=int, default=1, choices=[0, 1, 2],
@@ -520,6 +522,8 @@ def main():
     _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
     if a.gemm_stage >= 0:
         _lib.check(lib.admmq_debug_set_gemm_stage(a.gemm_stage), "gemm_stage")
+    if a.wide_min >= 0:
+        _lib.check(lib.admmq_debug_set_wide_min_tiles(a.wide_min), "wide_min")
     _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
     if a.f32_kernel >= 0:
         _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")

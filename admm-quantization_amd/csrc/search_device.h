@@ -98,22 +98,51 @@ __device__ __forceinline__ void hist_insert_elem(float x, const float* thr, int 
   full1 += af * (unsigned long long)kfull;
   full2 += (unsigned)(kfull * kfull);              // sum_{k<=kfull} (2k-1)
   unsigned slow = 0u;
+  if constexpr (QMAX <= 8) {
+    // every level's estimate and its two neighbouring thresholds first, so the 2 QMAX LDS
+    // reads are in flight together (read at their compare, each was waited for on its
+    // own), then the compares, then the adds (QMAX = 16 keeps the per-level form: the
+    // batched form's 32 reads spill in the thin loop)
+    int bk[QMAX];
+    float tlo[QMAX], thi[QMAX];
 #pragma unroll
-  for (int k = 1; k <= QMAX; ++k) {
-    const bool act = (k > kfull && k <= k0);
-    const float tau = a * ((float)(2 * QMAX - 1) / (float)(2 * k - 1));   // estimate only
-    const float ce = (tau - S0) * inv_step;
-    int b = (ce >= (float)(n - 1)) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
-    b = max(min(b, n - 1), 1);
-    const float* tk = thr + (k - 1) * n;
-    const bool exact = (a >= tk[b - 1]) && (a < tk[b]);
-    const bool add = act && exact;
-    slow |= (act && !exact) ? (1u << k) : 0u;
-    // only the lanes whose level k is active add (1-2 of the QMAX levels of an element):
-    // the masked-off lanes cost no LDS atomic (the former private dummy bins did)
-    if (add) {
-      atomicAdd(&h1[b], af);
-      atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+    for (int k = 1; k <= QMAX; ++k) {
+      const float tau = a * ((float)(2 * QMAX - 1) / (float)(2 * k - 1));   // estimate only
+      const float ce = (tau - S0) * inv_step;
+      int b = (ce >= (float)(n - 1)) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
+      b = max(min(b, n - 1), 1);
+      bk[k - 1] = b;
+      const float* tk = thr + (k - 1) * n;
+      tlo[k - 1] = tk[b - 1];
+      thi[k - 1] = tk[b];
+    }
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k) {
+      const bool act = (k > kfull && k <= k0);
+      const bool exact = (a >= tlo[k - 1]) && (a < thi[k - 1]);
+      slow |= (act && !exact) ? (1u << k) : 0u;
+      // only the lanes whose level k is active add (1-2 of the QMAX levels of an
+      // element): the masked-off lanes cost no LDS atomic
+      if (act && exact) {
+        atomicAdd(&h1[bk[k - 1]], af);
+        atomicAdd(&h2[bk[k - 1]], (unsigned)(2 * k - 1));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 1; k <= QMAX; ++k) {
+      const bool act = (k > kfull && k <= k0);
+      const float tau = a * ((float)(2 * QMAX - 1) / (float)(2 * k - 1));   // estimate only
+      const float ce = (tau - S0) * inv_step;
+      int b = (ce >= (float)(n - 1)) ? n - 1 : (ce < 0.f ? 1 : (int)ce + 1);
+      b = max(min(b, n - 1), 1);
+      const float* tk = thr + (k - 1) * n;
+      const bool exact = (a >= tk[b - 1]) && (a < tk[b]);
+      slow |= (act && !exact) ? (1u << k) : 0u;
+      if (act && exact) {
+        atomicAdd(&h1[b], af);
+        atomicAdd(&h2[b], (unsigned)(2 * k - 1));
+      }
     }
   }
   (void)dummy;

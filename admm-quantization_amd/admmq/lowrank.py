@@ -10,11 +10,12 @@ rho, max_iter, eps)`` (``:85-101``) with the other part held fixed.
   host round trip each (the reference syncs every iteration); the loop polls the flag
   every ``poll`` iterations to stop queueing early.
 * The quantization projection is the HIP quantizer (``admmq.quantize_tensor``).
-* The rank projection is ``project_rank`` (exact truncated SVD, the reference's
-  semantics), ``KrylovProjector`` (warm-started block Krylov in float64 that stops at a
-  residual bound: agrees with the exact truncation to ~1e-4 also on the flat spectra of
-  the loop's iterates) or ``SubspaceProjector`` (warm-started subspace iteration: cheaper,
-  but it stalls on flat spectra - kept for comparison).
+* The rank projection is ``KrylovProjector`` by default (warm-started block Krylov in
+  float64 on the hand-written panel kernels, stops at a residual bound: agrees with the
+  exact truncation to ~1e-4 also on the flat spectra of the loop's iterates),
+  ``project_rank`` (exact truncated SVD through the library, the reference's semantics;
+  ``projection="svd"``) or ``SubspaceProjector`` (warm-started subspace iteration:
+  cheaper, but it stalls on flat spectra - kept for comparison).
 """
 from __future__ import annotations
 
@@ -235,10 +236,16 @@ def admm_iteration(H: torch.Tensor, U: torch.Tensor, W: torch.Tensor, H2: torch.
 
 
 def factorize_lowrank(W: torch.Tensor, bits: int, rank: int, qscheme: str = "tensor_minmax", max_iter: int = 100,
-                      inner_iter: int = 50, rho: float = 1.0, seed: int = 42, projection: str = "svd",
+                      inner_iter: int = 50, rho: float = 1.0, seed: int = 42, projection: str = "krylov",
                       log_every: int = 10, logger=None):
     """The alternating loop of scripts/factorize_lowrank.py:156-170 (init 'random').
-    Returns (W_q, W_r, rel_history). Random starts come from the CPU generator (seeded)."""
+    Returns (W_q, W_r, rel_history). Random starts come from the CPU generator (seeded).
+
+    ``projection`` picks the rank projection (``:80-82``): ``"krylov"`` (default) is the
+    device block-Krylov projector on the hand-written fp64-MFMA panel kernels (DESIGN.md
+    §2.18; pinned to the reference's own trajectory band F10); ``"svd"`` is the exact
+    library SVD truncation (``project_rank``, the reference's arithmetic) for callers that
+    want it explicitly; ``"subspace"`` the cheaper subspace iteration (comparison only)."""
     _lib.require_device(W)
     dev = W.device
     g = torch.Generator().manual_seed(seed)
@@ -280,7 +287,9 @@ def main(argv=None):
     ap.add_argument("--qscheme", type=str, default="tensor_minmax")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--weights", type=str, default=None)
-    ap.add_argument("--projection", choices=["svd", "krylov", "subspace"], default="svd")
+    ap.add_argument("--projection", choices=["svd", "krylov", "subspace"], default="krylov",
+                    help="rank projection: device block-Krylov on the panel kernels (default) or the exact library "
+                         "SVD truncation of the reference (svd)")
     a = ap.parse_args(argv)
     if not torch.cuda.is_available():
         raise RuntimeError("admmq.lowrank needs a ROCm GPU")

@@ -8,23 +8,36 @@ fallback: the HIP library must be loaded.
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
 from . import _lib
 
-_WS: Dict[torch.device, torch.Tensor] = {}
-_GWS: Dict[torch.device, torch.Tensor] = {}
+# Workspaces keyed by (device, stream): the panel kernels' cross-workgroup partials and
+# arrival counters (which only count up; the workgroup that finishes a tile is the one whose
+# add completes a multiple of the group size) require every call on one workspace to be
+# stream-ordered (include/admmq.h). One workspace per stream keeps calls on different
+# streams from racing on the same slots and counters. A workspace is allocated on its own
+# stream, so when it is grown the caching allocator reuses the old block only for later work
+# of that same stream - never while another stream's kernel may still read it.
+_WS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+_GWS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+
+
+def _key(dev: torch.device) -> Tuple[torch.device, int]:
+    return (dev, int(torch.cuda.current_stream(dev).cuda_stream))
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
-    """The partials / arrival counters of the panel kernels, per device, grown on demand and
-    zeroed when (re)allocated (the counters must start at a multiple of the group size)."""
-    ws = _WS.get(dev)
+    """The partials / arrival counters of the panel kernels, per (device, current stream),
+    grown on demand and zeroed when (re)allocated (the counters must start at a multiple of
+    the group size)."""
+    k = _key(dev)
+    ws = _WS.get(k)
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
-        _WS[dev] = ws
+        _WS[k] = ws
     return ws
 
 
@@ -100,10 +113,11 @@ def gram(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -
     C = out if out is not None else torch.empty(p, q, dtype=torch.float64, device=A.device)
     lib = _lib.load()
     nb = lib.admmq_gram64_workspace_size(m, p, q)
-    ws = _GWS.get(A.device)
+    k = _key(A.device)
+    ws = _GWS.get(k)
     if ws is None or ws.numel() < nb:
         ws = torch.empty(max(int(nb), 256), dtype=torch.uint8, device=A.device)
-        _GWS[A.device] = ws
+        _GWS[k] = ws
     _lib.check(lib.admmq_gram64(_lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), m, p, q, _lib.ptr(C), _lib.ptr(ws),
                                 ws.numel(), _lib.stream_handle(A.device)), "gram64")
     return C

@@ -39,40 +39,63 @@ static int check_hip(const char* where) {
 // staging chunks, so that hipMemcpyAsync is truly asynchronous: a pageable source makes
 // the copy wait for the stream, which put every call's host planning on the GPU's
 // critical path (the host could not run ahead of the device by one mode call). A chunk
-// is reused once the event recorded after its copy has completed; one pool per device.
+// is reused once the event recorded after its copy has completed; one pool per device -
+// the device the STREAM belongs to (the event must be on it), not the caller's current
+// one. The pool is capped by bytes (kPinMaxBytes per device): when every chunk that could
+// hold the plan is still in flight and the cap is reached, the plan goes up by a plain
+// pageable hipMemcpyAsync instead (HIP stages a pageable source before it returns, so the
+// host buffer may be reused at once; that copy may wait for the stream - the only case in
+// which an entry point can block, include/admmq.h), never by waiting on a chunk's event.
 struct PinnedChunk { char* p; size_t cap; hipEvent_t ev; bool used; };
 static std::mutex g_pin_mu;
 static std::vector<PinnedChunk> g_pin[64];
-static constexpr size_t kPinMaxChunks = 256;
+static size_t g_pin_bytes[64];
+static constexpr size_t kPinMaxBytes = size_t(64) << 20;
 int upload_async(void* dst, const void* src, size_t n, hipStream_t s) {
   if (n == 0) return ADMMQ_OK;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int dev = -1;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+    (void)hipGetLastError();
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  if (dev < 0 || dev >= 64) dev = 0;
   std::lock_guard<std::mutex> g(g_pin_mu);
   std::vector<PinnedChunk>& pool = g_pin[dev];
   PinnedChunk* c = nullptr;
   for (PinnedChunk& k : pool)
     if (k.cap >= n && (!k.used || hipEventQuery(k.ev) == hipSuccess)) { c = &k; break; }
-  if (!c && pool.size() >= kPinMaxChunks) {   // all busy: wait for the oldest fitting one
-    for (PinnedChunk& k : pool)
-      if (k.cap >= n) { (void)hipEventSynchronize(k.ev); c = &k; break; }
+  size_t cap = 4096;
+  while (cap < n) cap *= 2;
+  if (!c && g_pin_bytes[dev] + cap > kPinMaxBytes) {   // pool full and busy: pageable copy
+    const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      g_err = std::string("upload (pageable): ") + hipGetErrorString(e);
+      return ADMMQ_ERR_HIP;
+    }
+    return ADMMQ_OK;
   }
   if (!c) {
     PinnedChunk k;
-    k.cap = 4096;
-    while (k.cap < n) k.cap *= 2;
+    k.cap = cap;
     k.used = false;
-    if (hipHostMalloc(reinterpret_cast<void**>(&k.p), k.cap, hipHostMallocDefault) != hipSuccess) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);   // the event (and the chunk's mapping) on the stream's device
+    const hipError_t ea = hipHostMalloc(reinterpret_cast<void**>(&k.p), k.cap, hipHostMallocDefault);
+    const hipError_t ee = ea == hipSuccess ? hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) : ea;
+    if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+    if (ea != hipSuccess) {
       (void)hipGetLastError();
       g_err = "upload: pinned staging allocation failed";
       return ADMMQ_ERR_HIP;
     }
-    if (hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess) {
+    if (ee != hipSuccess) {
       (void)hipHostFree(k.p);
       g_err = "upload: event creation failed";
       return ADMMQ_ERR_HIP;
     }
     pool.push_back(k);
+    g_pin_bytes[dev] += k.cap;
     c = &pool.back();
   }
   std::memcpy(c->p, src, n);

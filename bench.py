@@ -139,18 +139,23 @@ def run_step(work, max_iter_admm, num_attempts=200):
 USE_DIST = False   # torch.distributed (RCCL) on: world > 1, or --force-dist (exercises the collectives at N = 1)
 
 
-def gather_factors(runs, rank, world, numel, device):
+def gather_factors(runs, rank, world, numel, device, keep=None):
     """The single collective of the path: every rank's converged factors to rank 0 (one
     RCCL gather over xGMI). Sizes are static (numel from the shard plan), so the flat
-    buffers are padded to the largest rank's size and no size exchange is needed."""
+    buffers are padded to the largest rank's size and no size exchange is needed. Returns
+    the element count rank 0 holds; `keep` (a list) receives rank 0's per-rank buffers."""
     flat = torch.cat([f.reshape(-1) for r in runs for f in r.factors]) if runs else torch.zeros(0, device=device)
     assert flat.numel() == numel[rank], (flat.numel(), numel[rank])
     if world == 1 and not USE_DIST:
+        if keep is not None:
+            keep[:] = [flat]
         return flat.numel()
     buf = torch.zeros(max(numel), device=device)
     buf[:flat.numel()] = flat
     out = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
     dist.gather(buf, out, dst=0)
+    if keep is not None and rank == 0:
+        keep[:] = [out[k][:numel[k]] for k in range(world)]
     return sum(numel)
 
 
@@ -445,6 +450,60 @@ def emulate_shards(a):
     print(json.dumps(out), flush=True)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` (no WORLD_SIZE): run the same command under
+    torch.distributed.run with N ranks on this node (rendezvous on 127.0.0.1) as a CHILD
+    process - this parent never initialises the GPU, so no exec from a GPU process - relay
+    its output and exit with its code. Rank 0 prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def dry_run(a, world, rank):
+    """--cpu-dry-run: the multi-rank plumbing of a real run on CPU tensors over gloo - the
+    LPT shard plan, warmup + K timed (kernel-free) steps between barriers, the single factor
+    gather to rank 0 and the max / sum reductions - so a CPU test can check that `--gpus N`
+    forms N ranks and that rank 0 receives every layer's factors."""
+    device = torch.device("cpu")
+    if USE_DIST:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    work, numel, shard_info = build_workload(a.model, rank, world, a.shard, device)
+    got, keep = 0, []
+    t0 = time.perf_counter()
+    for _ in range(a.warmup + a.steps):
+        runs = [type("Run", (), {"factors": [f.clone() for f in init]})() for (_, _, _, init) in work]
+        got = gather_factors(runs, rank, world, numel, device, keep)
+    if USE_DIST:
+        dist.barrier()
+    elapsed, nfi = reduce_over_ranks(time.perf_counter() - t0, len(work), world, device)
+    if rank == 0:
+        # every rank's gathered buffer equals that rank's own factors (here: its seeded init)
+        match = []
+        for k in range(world):
+            wk, _, _ = build_workload(a.model, k, world, a.shard, device)
+            ref = torch.cat([f.reshape(-1) for (_, _, _, init) in wk for f in init]) if wk else torch.zeros(0)
+            match.append(bool(torch.equal(keep[k], ref)))
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_formed": world, "gathered_elements": got,
+                          "expected_elements": sum(numel), "layers_total": int(nfi),
+                          "layers_per_rank": (shard_info or {}).get("layers_per_rank"),
+                          "rank_factors_match": match, "elapsed_s": elapsed}), flush=True)
+    if USE_DIST:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -497,19 +556,34 @@ def main():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="tests only: no GPU, no kernels - the launcher, the shard plan and the factor gather over "
+                         "gloo on CPU tensors (the factors are the init, unchanged)")
     a = ap.parse_args()
     if a.emulate_world > 0:
         return emulate_shards(a)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # --gpus N without a launcher: start N rank processes as children (torch.distributed.run);
+        # this process never touches the GPU (no exec from a GPU-initialised process)
+        return launch_ranks(a.gpus)
+    world = int(env_world or "1")
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher formed WORLD_SIZE={world}; refusing to report a "
+              f"{world}-rank run as {a.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
     global USE_DIST
     USE_DIST = world > 1 or a.force_dist
+    if a.cpu_dry_run:
+        return dry_run(a, world, rank)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
     if USE_DIST:
         dist.init_process_group("nccl", device_id=device)
+        world = dist.get_world_size()   # n_gpus from the world actually formed
 
     from admmq import _lib
     lib = _lib.load()

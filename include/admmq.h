@@ -6,8 +6,11 @@
  * buffers, uses only caller-owned workspace, and returns an int32 status
  * (ADMMQ_OK = 0). No entry point allocates device memory or synchronises with the
  * device: plans (descriptor and work-unit tables) go up with hipMemcpyAsync from a pool
- * of pinned host staging chunks the library grows on first use and reuses once their
- * copies have completed, so a call returns while its launches are still queued.
+ * of pinned host staging chunks (per device of the stream, at most 64 MB) the library
+ * grows on first use and reuses once their copies have completed, so a call returns
+ * while its launches are still queued. Only when every chunk is in flight and the pool
+ * is at its cap does a plan go up from pageable memory, a copy that may wait for the
+ * stream (it never waits on the device otherwise).
  *
  * Reference interfaces replaced (KamikaziZen/admm-quantization @ 2024_10_08):
  *   admmq_admm_prepare + admmq_admm_run  <- source/admm.py:51-67  admm_iteration(H,U,F,G,max_iter,eps,bits,qscheme)

@@ -112,3 +112,39 @@ def test_lpt_balance():
     assert abs(loads[0] - loads[1]) <= biggest
     with pytest.raises(KeyError):
         owner[len(specs)]
+
+
+def _bench_cli(*args, env_extra=None, timeout=300):
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("model", ["resnet18", "resnet50"])
+def test_bench_gpus_flag_launches_ranks(model):
+    """`python bench.py --gpus 2` with no launcher starts 2 rank processes itself (torch.
+    distributed.run as a child of a parent that never touches the GPU): the
+    line reports the 2 ranks actually formed, and rank 0's single gather holds every
+    rank's factors (checked element for element against each rank's own factors)."""
+    rc, line, err = _bench_cli("--gpus", "2", "--cpu-dry-run", "--steps", "1", "--warmup", "1", "--model", model)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["ranks_formed"] == 2
+    assert line["gathered_elements"] == line["expected_elements"]
+    assert line["rank_factors_match"] == [True, True]
+    assert sum(line["layers_per_rank"]) == line["layers_total"] == (16 if model == "resnet18" else 48)
+
+
+def test_bench_gpus_one_unchanged_and_mismatch_refused():
+    """--gpus 1 runs in-process (no launcher); a --gpus that disagrees with the launcher's
+    WORLD_SIZE exits non-zero instead of reporting the wrong rank count."""
+    rc, line, err = _bench_cli("--gpus", "1", "--cpu-dry-run", "--steps", "1", "--warmup", "0")
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 1 and line["rank_factors_match"] == [True]
+    rc, line, err = _bench_cli("--gpus", "4", "--cpu-dry-run", env_extra={"WORLD_SIZE": "2"})
+    assert rc == 2 and line is None and "refusing" in err

@@ -156,6 +156,17 @@ def test_c4_fused_three_groups_equals_separate(torch_dev):
     assert (ia[:, 3] == 0).all() and (ia[:, 4] == 0).all() and np.array_equal(ia[:, :3], ib[:, :3])
     for (ha, ua), (hb, ub), pr in zip(a, b, probs):
         assert np.array_equal(_bits(ha), _bits(hb)) and np.array_equal(_bits(ua), _bits(ub)), pr[0]
+    # the three-group plan without the fused finalize (the fault-repair re-run's form: non-fused
+    # k_mse_hist3<.., 3, false> with several units per block + k_finalize_admm), and the
+    # exhaustive sweep under the same plan (k_mse_hist<.., 3>): the same bits (advisor r04)
+    c, ic = run(True, False)
+    with _lib.exhaustive_search(True):
+        e, ie = run(True, False)
+    for info in (ic, ie):
+        assert np.array_equal(info[:, :3], ib[:, :3])
+    for (hc, uc), (he, ue), (hb, ub), pr in zip(c, e, b, probs):
+        assert np.array_equal(_bits(hc), _bits(hb)) and np.array_equal(_bits(uc), _bits(ub)), pr[0]
+        assert np.array_equal(_bits(he), _bits(hb)) and np.array_equal(_bits(ue), _bits(ub)), pr[0]
 
 
 def _llama_problem(torch, dev, I, J, R, seed):

@@ -114,11 +114,15 @@ def test_krylov_projector_on_the_loops_flat_spectrum_iterate(env):
             assert rel < 1e-4, (gap, rel, P.blocks)
 
 
+@pytest.mark.parametrize("projection", [None, "svd"])
 @pytest.mark.parametrize("qs", ["tensor_minmax", "tensor_mseminmax_symmetric"])
-def test_outer_loop_matches_reference(env, qs):
+def test_outer_loop_matches_reference(env, qs, projection):
+    """The drop-in's default (projection=None: the device Krylov projector on the panel
+    kernels) and the explicit exact-SVD projection both follow the reference's F6 outer loop."""
     torch, dev, z = env
     from admmq.lowrank import factorize_lowrank
-    Wq, Wr, hist = factorize_lowrank(_t(torch, dev, z["W"]), 4, 4, qs, max_iter=3, seed=42)
+    kw = {} if projection is None else {"projection": projection}
+    Wq, Wr, hist = factorize_lowrank(_t(torch, dev, z["W"]), 4, 4, qs, max_iter=3, seed=42, **kw)
     ref = z[f"{qs}_outer_rel"]
     np.testing.assert_allclose(hist, ref, rtol=1e-3)
     assert _rel(Wr.cpu().numpy(), z[f"{qs}_outer_Wr"]) < 1e-2

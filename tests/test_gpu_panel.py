@@ -139,3 +139,32 @@ def test_panel_argument_errors(env):
         panel.xy(X.double(), torch.zeros(8, 4, dtype=torch.float64, device=dev))
     with pytest.raises(Exception):
         panel.outer(torch.zeros(4, 40, dtype=torch.float64, device=dev), torch.zeros(4, 40, dtype=torch.float64, device=dev))
+
+
+def test_two_streams_own_workspaces(env):
+    """Panel calls queued on two streams at once (advisor r04: one shared workspace let
+    their partial slots and monotonic arrival counters race) each get their own (device,
+    stream) workspace: every product equals the single-stream result bit for bit, and a
+    later call on the default stream is still correct (counters stayed in step)."""
+    torch, dev = env
+    from admmq import panel
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(2048, 1536, generator=g).to(dev)
+    Qs = [torch.randn(2048, 32, generator=g, dtype=torch.float64).to(dev) for _ in range(2)]
+    Ys = [torch.randn(1536, 32, generator=g, dtype=torch.float64).to(dev) for _ in range(2)]
+    ref_t = [panel.xtq(X, Q) for Q in Qs]
+    ref_y = [panel.xy(X, Y) for Y in Ys]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    outs = [[], []]
+    for rep in range(8):
+        for j, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                outs[j].append((panel.xtq(X, Qs[j]), panel.xy(X, Ys[j])))
+    torch.cuda.synchronize()
+    for j in range(2):
+        for t, y in outs[j]:
+            assert torch.equal(t, ref_t[j]) and torch.equal(y, ref_y[j])
+    keys = {k for k in panel._WS if k[0] == dev}
+    assert len(keys) >= 3   # the default stream and the two side streams
+    assert torch.equal(panel.xtq(X, Qs[0]), ref_t[0])

@@ -133,3 +133,42 @@ def epc_mu(c: torch.Tensor, s: torch.Tensor, normY2: float, delta2: float) -> to
     _lib.check(_lib.load().admmq_epc_mu(_lib.ptr(c), _lib.ptr(s), c.numel(), float(normY2), float(delta2), _lib.ptr(mu),
                                         _lib.stream_handle(c.device)), "epc_mu")
     return mu
+
+
+SPD_SMALL_MAX = 140   # n of the one-workgroup fp64 solves (csrc/epc_kernels.hip: the matrix in LDS)
+
+
+def spd_solve64(G: torch.Tensor, F: torch.Tensor) -> torch.Tensor:
+    """``F G^-1`` (m x n float64) for SPD ``G`` (n x n, n <= SPD_SMALL_MAX) on the device: the
+    CP-ALS update ``torch.linalg.solve(G, F.T).T`` of tensorly ``parafac`` (one workgroup,
+    Cholesky in LDS, no host synchronisation; a non-SPD G gives NaN rows instead of raising)."""
+    n = G.shape[0]
+    if G.dtype != torch.float64 or F.dtype != torch.float64 or G.shape != (n, n) or F.dim() != 2 or F.shape[1] != n:
+        raise ValueError("admmq.panel.spd_solve64: G (n x n) and F (m x n) must be float64")
+    if n > SPD_SMALL_MAX:
+        raise ValueError(f"admmq.panel.spd_solve64: n = {n} > {SPD_SMALL_MAX}")
+    G, F = G.contiguous(), F.contiguous()
+    X = torch.full(F.shape, float("nan"), dtype=torch.float64, device=F.device)
+    _lib.check(_lib.load().admmq_spd_solve64(_lib.ptr(G), _lib.ptr(F), F.shape[0], n, _lib.ptr(X), None,
+                                             _lib.stream_handle(F.device)), "spd_solve64")
+    return X
+
+
+def epc_step64(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor) -> torch.Tensor:
+    """One EPC mode update of musco ``cp_anc`` on the device: ``F (G + mu I)^-1`` with ``mu >= 0``
+    the root of the error equation (``csrc/epc_kernels.hip``: Newton steps on Cholesky factors
+    of ``G + mu I``, no eigendecomposition). ``mu`` is a 0-dim float64 device tensor: the warm
+    start in, the root out (updated in place). n <= SPD_SMALL_MAX; no host synchronisation."""
+    n = G.shape[0]
+    if G.dtype != torch.float64 or F.dtype != torch.float64 or G.shape != (n, n) or F.dim() != 2 or F.shape[1] != n:
+        raise ValueError("admmq.panel.epc_step64: G (n x n) and F (m x n) must be float64")
+    if n > SPD_SMALL_MAX:
+        raise ValueError(f"admmq.panel.epc_step64: n = {n} > {SPD_SMALL_MAX}")
+    if mu.dtype != torch.float64 or mu.numel() != 1 or mu.device != F.device:
+        raise ValueError("admmq.panel.epc_step64: mu must be a float64 scalar tensor on F's device")
+    G, F = G.contiguous(), F.contiguous()
+    X = torch.empty(F.shape, dtype=torch.float64, device=F.device)
+    _lib.check(_lib.load().admmq_epc_step64(_lib.ptr(G), _lib.ptr(F), F.shape[0], n, float(normY2), float(delta2),
+                                            _lib.ptr(mu), _lib.ptr(X), None, _lib.stream_handle(F.device)),
+               "epc_step64")
+    return X

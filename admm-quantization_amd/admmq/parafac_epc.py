@@ -21,10 +21,14 @@ Device placement: every per-mode MTTKRP and Gram-Hadamard product (the O(I J K R
 runs on the fp64 HIP kernels (``als.gram_mttkrp_f64`` -> ``csrc/cp64_kernels.hip``, f64
 MFMA with the Khatri-Rao operand formed on the fly); the reconstruction errors use the
 CP identity ||Y||^2 - 2 <Y, [[w; U]]> + ||[[w; U]]||^2 on those products (no I x J x K
-reconstruction, as tensorly's ``parafac`` does); the R x R solves / eigendecompositions
-are torch linear algebra on the device, and the EPC step's scalar root search for mu runs
-on the device as well (``panel.epc_mu``, ``csrc/epc_kernels.hip``: no host synchronisation
-per mode step).
+reconstruction, as tensorly's ``parafac`` does); the R x R solves run on one workgroup with
+the matrix in LDS (``panel.spd_solve64`` for the CP-ALS update, ``panel.epc_step64`` for the
+EPC update: Cholesky factors of G + mu I and Newton steps on the error equation instead of
+an eigendecomposition; ``csrc/epc_kernels.hip``) for R <= 140, torch linear algebra above
+that. The stopping scalars stay on the device: the drivers run ``_CHECK_EVERY`` iterations
+between host reads, keep each iteration's factors, and on a stop return those of the
+iteration the reference would have stopped at (the same iterations and results as a
+per-iteration check, without its host synchronisation).
 Float64 tensors on the GPU only: a CPU tensor raises (no CPU path).
 """
 from __future__ import annotations
@@ -34,7 +38,9 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from .als import gram_mttkrp_f64
-from .panel import epc_mu
+from .panel import SPD_SMALL_MAX, epc_mu, epc_step64, spd_solve64
+
+_CHECK_EVERY = 8   # iterations between the host's reads of the device-side stop tests
 
 
 def _khatri_rao(mats: List[torch.Tensor]) -> torch.Tensor:
@@ -58,14 +64,22 @@ def _on_gpu64(tensor) -> torch.Tensor:
     return X.to(torch.float64)
 
 
-def _cp_error2(normY2: float, F_last: torch.Tensor, G_last: torch.Tensor, U_last: torch.Tensor,
-               weights: Optional[torch.Tensor] = None) -> float:
-    """||Y - [[w; U]]||^2 from the last mode's MTTKRP F and Gram-Hadamard G (of the other
-    factors) and its factor: ||Y||^2 - 2 <F, U w> + w^T (G * U^T U) w."""
+def _cp_error2(normY2, F_last: torch.Tensor, G_last: torch.Tensor, U_last: torch.Tensor,
+               weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """||Y - [[w; U]]||^2 (a 0-dim device tensor: no host synchronisation) from the last
+    mode's MTTKRP F and Gram-Hadamard G (of the other factors) and its factor:
+    ||Y||^2 - 2 <F, U w> + w^T (G * U^T U) w."""
     Uw = U_last * weights if weights is not None else U_last
-    inner = float(torch.sum(F_last * Uw))
-    norm2 = float(torch.sum(G_last * (Uw.T @ Uw)))
-    return max(normY2 - 2.0 * inner + norm2, 0.0)
+    inner = torch.sum(F_last * Uw)
+    norm2 = torch.sum(G_last * (Uw.T @ Uw))
+    return torch.clamp(normY2 - 2.0 * inner + norm2, min=0.0)
+
+
+def _als_update(G: torch.Tensor, F: torch.Tensor) -> torch.Tensor:
+    """tensorly parafac's factor update U = F G^-1 (G = Hadamard of the other Grams)."""
+    if G.shape[0] <= SPD_SMALL_MAX:
+        return spd_solve64(G, F)
+    return torch.linalg.solve(G, F.T).T
 
 
 def parafac(tensor: torch.Tensor, rank: int, init: str = "random", random_state=None, tol: float = 1e-8,
@@ -78,17 +92,30 @@ def parafac(tensor: torch.Tensor, rank: int, init: str = "random", random_state=
     if init != "random":
         raise NotImplementedError(f"parafac init={init!r}")
     fs = [torch.rand(X.shape[m], rank, generator=gen, dtype=torch.float64).to(X.device) for m in range(n)]
-    normY2 = float(torch.sum(X * X))
-    norm_x = normY2 ** 0.5
+    normY2 = torch.sum(X * X)
+    norm_x = torch.sqrt(normY2)
     prev = None
-    for _ in range(n_iter_max):
-        for m in range(n):
-            F, G = gram_mttkrp_f64(X, fs, m)
-            fs[m] = torch.linalg.solve(G, F.T).T
-        err = _cp_error2(normY2, F, G, fs[n - 1]) ** 0.5 / norm_x   # F, G of the last mode
-        if prev is not None and abs(prev - err) < tol:
+    it = 0
+    while it < n_iter_max:
+        # a chunk of iterations between host reads: every iteration's factors and error kept
+        snaps, errs = [], []
+        for _ in range(min(_CHECK_EVERY, n_iter_max - it)):
+            for m in range(n):
+                F, G = gram_mttkrp_f64(X, fs, m)
+                fs[m] = _als_update(G, F)
+            errs.append(torch.sqrt(_cp_error2(normY2, F, G, fs[n - 1])) / norm_x)   # F, G of the last mode
+            snaps.append(list(fs))
+        it += len(errs)
+        ev = torch.stack(errs).tolist()   # the chunk's one host read
+        stop = None
+        for k, err in enumerate(ev):
+            if prev is not None and abs(prev - err) < tol:
+                stop = k
+                break
+            prev = err
+        if stop is not None:
+            fs = snaps[stop]
             break
-        prev = err
     weights = torch.ones(rank, dtype=torch.float64, device=X.device)
     if normalize_factors:
         for m in range(n):
@@ -96,6 +123,17 @@ def parafac(tensor: torch.Tensor, rank: int, init: str = "random", random_state=
             weights = weights * nrm
             fs[m] = fs[m] / nrm
     return weights, fs
+
+
+def _epc_update(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor) -> torch.Tensor:
+    """cp_anc's mode update U_n = F (G + mu I)^-1 with mu on the error equation."""
+    if G.shape[0] <= SPD_SMALL_MAX:
+        return epc_step64(G, F, normY2, delta2, mu)
+    s, V = torch.linalg.eigh(G)
+    s = s.clamp_min(0.0)
+    Ft = F @ V
+    mu.copy_(epc_mu(torch.sum(Ft * Ft, dim=0), s, normY2, delta2))   # on the device: no host sync
+    return (Ft / (s + mu).clamp_min(1e-300)) @ V.T
 
 
 def cp_anc(tensor: torch.Tensor, rank: int, delta: float, weights: Optional[torch.Tensor] = None,
@@ -110,26 +148,34 @@ def cp_anc(tensor: torch.Tensor, rank: int, delta: float, weights: Optional[torc
         fs[-1] = fs[-1] * weights.to(fs[-1])
     normY2 = float(torch.sum(Y * Y))
     delta2 = float(delta) ** 2
+    mus = [torch.zeros((), dtype=torch.float64, device=Y.device) for _ in range(n)]   # warm starts per mode
     lam_prev = None
-    for _ in range(max(int(maxiter), 1)):
-        for m in range(n):
-            # normalise the other factors, moving their column norms into factor m
-            for k in range(n):
-                if k != m:
-                    nrm = torch.linalg.norm(fs[k], dim=0).clamp_min(1e-300)
-                    fs[k] = fs[k] / nrm
-                    fs[m] = fs[m] * nrm
-            F, G = gram_mttkrp_f64(Y, fs, m)
-            s, V = torch.linalg.eigh(G)
-            s = s.clamp_min(0.0)
-            Ft = F @ V
-            mu = epc_mu(torch.sum(Ft * Ft, dim=0), s, normY2, delta2)   # on the device: no host sync
-            fs[m] = (Ft / (s + mu).clamp_min(1e-300)) @ V.T
-        lam = torch.linalg.norm(fs[n - 1], dim=0)
-        lnorm = float(torch.linalg.norm(lam))
-        if lam_prev is not None and abs(lam_prev - lnorm) < tol * lam_prev:
+    it, total = 0, max(int(maxiter), 1)
+    while it < total:
+        snaps, lnorms = [], []
+        for _ in range(min(_CHECK_EVERY, total - it)):
+            for m in range(n):
+                # normalise the other factors, moving their column norms into factor m
+                for k in range(n):
+                    if k != m:
+                        nrm = torch.linalg.norm(fs[k], dim=0).clamp_min(1e-300)
+                        fs[k] = fs[k] / nrm
+                        fs[m] = fs[m] * nrm
+                F, G = gram_mttkrp_f64(Y, fs, m)
+                fs[m] = _epc_update(G, F, normY2, delta2, mus[m])
+            lnorms.append(torch.linalg.norm(torch.linalg.norm(fs[n - 1], dim=0)))
+            snaps.append(list(fs))
+        it += len(lnorms)
+        lv = torch.stack(lnorms).tolist()   # the chunk's one host read
+        stop = None
+        for k, lnorm in enumerate(lv):
+            if lam_prev is not None and abs(lam_prev - lnorm) < tol * lam_prev:
+                stop = k
+                break
+            lam_prev = lnorm
+        if stop is not None:
+            fs = snaps[stop]
             break
-        lam_prev = lnorm
     # final normalisation: every factor unit-norm columns, intensities in the weights
     weights = torch.ones(rank, dtype=torch.float64, device=Y.device)
     for m in range(n):
@@ -151,7 +197,7 @@ def parafac_epc(tensor, rank, als_maxiter=5000, als_tol=1e-5, num_threads=4, ini
     lmbda, fs = parafac(Y, rank, init=init, tol=als_tol, n_iter_max=als_maxiter, normalize_factors=True)
     last = Y.dim() - 1
     F, G = gram_mttkrp_f64(Y, fs, last)
-    delta = _cp_error2(float(torch.sum(Y * Y)), F, G, fs[last], lmbda) ** 0.5
+    delta = float(_cp_error2(torch.sum(Y * Y), F, G, fs[last], lmbda)) ** 0.5
     lambda_norm_prev = float(torch.linalg.norm(lmbda))
     alpha_prev = float(lmbda.max() / lmbda.min())
     stopflag = 0

@@ -290,6 +290,22 @@ int32_t admmq_gram64(const double* A, int64_t lda, const double* B, int64_t ldb,
 int32_t admmq_epc_mu(const double* c, const double* s, int64_t n, double normY2, double delta2, double* mu,
                      void* stream);
 
+/* The R x R solves of the CP-ALS / EPC initialiser on one workgroup (the fp64 matrix in LDS,
+ * 1 <= n <= 140), replacing tensorly parafac's torch.linalg.solve and cp_anc's eigendecomposition
+ * (source/parafac_epc.py:42, :61-74). Row-major device doubles; no host synchronisation.
+ *   admmq_spd_solve64  X = F G^-1 (F, X: m x n; G: n x n SPD); *info (device int, may be NULL)
+ *                      = 0, or 1 when G is not positive definite (X untouched).
+ *   admmq_epc_step64   X = F (G + mu I)^-1 with mu >= 0 the root of
+ *                      normY2 - <F, X> - mu ||X||^2 = delta2 (= the eigen form
+ *                      normY2 - sum_j |F v_j|^2 (s_j + 2 mu) / (s_j + mu)^2), 0 when the LS step's
+ *                      error already reaches delta2; *mu (device double): in, a warm start (<= 0:
+ *                      none), out, the root. *info (may be NULL): 0, or 1 when no G + mu I on the
+ *                      search bracket was positive definite. */
+int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n, double* X, int32_t* info,
+                          void* stream);
+int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
+                         double* mu, double* X, int32_t* info, void* stream);
+
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);
 const char* admmq_last_error(void);

@@ -115,3 +115,52 @@ def test_epc_mu_device_matches_oracle(R, seed):
         ref = eo._solve_mu(c, s, normY2, delta2)
         got = float(panel.epc_mu(c.cuda(), s.cuda(), normY2, delta2))
         assert abs(got - ref) <= 1e-12 * max(abs(ref), 1e-300) or (ref == 0.0 and got == 0.0), (delta2, got, ref)
+
+
+@pytest.mark.parametrize("n,m", [(1, 3), (5, 9), (64, 1), (134, 64), (134, 9), (140, 130)])
+def test_spd_solve64_vs_library(n, m):
+    """The one-workgroup fp64 solve (csrc/epc_kernels.hip: Cholesky with the matrix in LDS,
+    16-lane substitution groups) that replaces tensorly parafac's torch.linalg.solve
+    (source/parafac_epc.py:42): X = F G^-1 within 1e-11 of the float64 library solve on a
+    well-conditioned SPD G, at n up to the LDS limit and m above one pass of 64 rows."""
+    from admmq import panel
+    g = torch.Generator().manual_seed(n * 1000 + m)
+    B = torch.randn(n, 2 * n + 3, generator=g, dtype=torch.float64)
+    G = B @ B.T / (2 * n + 3) + 0.1 * torch.eye(n, dtype=torch.float64)
+    F = torch.randn(m, n, generator=g, dtype=torch.float64)
+    X = panel.spd_solve64(G.cuda(), F.cuda())
+    ref = torch.linalg.solve(G, F.T).T
+    assert _rel(X, ref) < 1e-11, _rel(X, ref)
+
+
+@pytest.mark.parametrize("n,m,seed", [(134, 64, 1), (134, 9, 2), (7, 5, 3), (140, 64, 4)])
+def test_epc_step64_vs_eigen_form(n, m, seed):
+    """The EPC mode update on the device (Newton on Cholesky factors of G + mu I, no
+    eigendecomposition) against the eigen form the oracle uses (oracle/epc_oracle.py:
+    eigh, mu by bisection to fp64 resolution, U = F V diag(1/(s + mu)) V^T) in float64 on
+    the CPU: mu and U within 1e-9, for targets needing mu > 0 (with and without a warm
+    start) and for one the least-squares step already meets (mu = 0)."""
+    from admmq import panel
+    g = torch.Generator().manual_seed(seed)
+    B = torch.randn(n, n + 8, generator=g, dtype=torch.float64)
+    G = B @ B.T / (n + 8) + 1e-3 * torch.eye(n, dtype=torch.float64)
+    F = torch.randn(m, n, generator=g, dtype=torch.float64)
+    s, V = torch.linalg.eigh(G)
+    s = s.clamp_min(0.0)
+    Ft = F @ V
+    c = torch.sum(Ft * Ft, dim=0)
+    ls = float(torch.sum(c / s))            # <F, F G^-1>: e(0) = normY2 - ls
+    normY2 = ls * 1.5
+    e0 = normY2 - ls
+    # (normY2 = 3 e0, so delta2 < normY2: a finite root)
+    for delta2, warm in ((e0 * 1.5, 0.0), (e0 * 2.5, 0.0), (e0 * 2.5, 0.37 * float(s.mean())), (e0 * 0.5, 0.0)):
+        ref_mu = eo._solve_mu(c, s, normY2, delta2)
+        ref_X = (Ft / (s + ref_mu).clamp_min(1e-300)) @ V.T
+        mu = torch.tensor(warm, dtype=torch.float64, device="cuda")
+        X = panel.epc_step64(G.cuda(), F.cuda(), normY2, delta2, mu)
+        got = float(mu)
+        if ref_mu == 0.0:
+            assert got == 0.0
+        else:
+            assert abs(got - ref_mu) <= 1e-8 * ref_mu, (delta2, warm, got, ref_mu)
+        assert _rel(X, ref_X) < 1e-9, (delta2, warm, _rel(X, ref_X))

@@ -2,20 +2,25 @@
 iterations per mode call, scripts/factorize.py:218-221) with eps = 0, the schedule
 bench.py times. Shorter-horizon parity (one step bit-level, 30 steps at the largest R,
 the 20 x 20 ALS band) is in test_gpu_parity.py; here the contract is what survives 999
-chaotic iterations (the reference is not reproducible against itself at
-this horizon, F4 / F8):
+chaotic iterations. The reference is not reproducible against itself at this horizon
+(SURVEY.md §0, F8): F11 (tests/golden/gen_f11_horizon.py) re-ran the reference's own
+admm_iteration on C2 from the same start with its cholesky_solve moved by <= 1 ulp, and
+its objective ||F - H G|| / ||F|| spreads over ~2 % (mode 0: 0.1582 ... 0.1610), so the
+contract is that band (widened by half its width, the F10 rule), not a 1e-3 match to any
+one run:
 
   * C2 (resnet18 layer1.0.conv1, every mode from the same seed-42 start, F and G from the
-    oracle): the objective ||F - H G|| / ||F|| of the 999-iteration result against the CPU
-    oracle's run of the same call (per-iteration Cholesky solve, source/admm.py:54-56)
-    within 1e-3 relative, the same iteration count, every result on a 4-bit grid
-    (<= 16 levels) whose step agrees with the oracle's within 5 %;
+    oracle): the 999-iteration result's objective inside the reference's F11 band, the
+    reference's iteration count, every result on a 4-bit grid (<= 16 levels) whose step is
+    inside the band of the reference's grid steps; the CPU oracle's run of the same call is
+    printed beside it;
   * C2 as one ALS sweep (the three modes in sequence, the reference loop): the sweep's
-    reconstruction errors (rec_error, quant_rec_error) against the oracle's sweep within 2 %;
+    reconstruction errors (rec_error, quant_rec_error) inside the reference's F11 sweep band;
   * C3 (all 16 resnet18 3x3 convs batched, the bench's step): property checks on every
     (layer, mode) - 999 iterations each, finite factors on <= 16 levels, finite losses
     below the random start's, no fused-path fault repaired.
 """
+import json
 import os
 
 import numpy as np
@@ -28,6 +33,14 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 
 MSE = "tensor_mseminmax_symmetric"
 MAX_ITER = 1000   # the bench's max_iter_admm: 999 inner iterations
+F11 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f11_horizon.json")
+
+
+def _band(vals):
+    """[min, max] of the reference's runs widened by half the width on each side (F10's rule)."""
+    lo, hi = min(vals), max(vals)
+    w = 0.5 * (hi - lo)
+    return lo - w, hi + w
 
 
 @pytest.fixture(scope="module")
@@ -67,39 +80,46 @@ def _objective(F, G, h):
 def test_c2_mode_call_at_bench_horizon(torch_dev, mode):
     torch, dev = torch_dev
     from admmq import admm_iteration_batched
+    ref = json.load(open(F11))["modes"][str(mode)]
     W, R, fs = _c2_start()
     G, F = ao.gram_mttkrp(W, fs, mode)
     H0 = fs[mode]
-    Ho, Uo, oinfo = ao.admm_iteration(H0, np.zeros_like(H0), F, G, MAX_ITER, 0.0, 4, MSE, return_info=True)
     p = (_t(torch, dev, H0), torch.zeros(H0.shape, device=dev), _t(torch, dev, F), _t(torch, dev, G))
     (H,), info = admm_iteration_batched([p], MAX_ITER, 0.0, 4, MSE, return_info=True)
     H, U = H.cpu().numpy(), p[1].cpu().numpy()
-    assert int(info[0, 0]) == oinfo["iters"] == MAX_ITER - 1
+    assert int(info[0, 0]) == MAX_ITER - 1   # eps = 0: the reference runs every iteration
     assert int(info[0, 2]) == 0 and int(info[0, 3]) == 0   # no SPD error, no internal fault
     assert np.all(np.isfinite(U))
-    og, oo = _objective(F, G, H), _objective(F, G, Ho)
-    sg, so = _levels(H), _levels(Ho)
-    print(f"C2 mode {mode}, {MAX_ITER - 1} its: objective gpu {og:.6e} oracle {oo:.6e} ({abs(og - oo) / oo:.2e}), "
-          f"grid step {sg:.4e} / {so:.4e}, H entries differing {float(np.mean(H != Ho)):.2e}")
-    assert abs(og - oo) / oo < 1e-3
-    assert abs(sg - so) / so < 0.05
+    og, sg = _objective(F, G, H), _levels(H)
+    Ho, _, oinfo = ao.admm_iteration(H0, np.zeros_like(H0), F, G, MAX_ITER, 0.0, 4, MSE, return_info=True)
+    assert oinfo["iters"] == MAX_ITER - 1
+    lo, hi = _band(ref["objective"])
+    slo, shi = _band(ref["grid_step"])
+    print(f"C2 mode {mode}, {MAX_ITER - 1} its: objective gpu {og:.6e}, oracle {_objective(F, G, Ho):.6e}, "
+          f"reference runs {min(ref['objective']):.6e} .. {max(ref['objective']):.6e}; grid step gpu {sg:.4e}, "
+          f"reference {min(ref['grid_step']):.4e} .. {max(ref['grid_step']):.4e}")
+    assert lo <= og <= hi, (og, lo, hi)
+    assert slo <= sg <= shi, (sg, slo, shi)
 
 
 def test_c2_sweep_at_bench_horizon(torch_dev):
     torch, dev = torch_dev
     from admmq.factorize import LayerRun, als_sweep
+    ref = json.load(open(F11))["sweep"]
     W, R, fs = _c2_start()
-    _, _, loss, lossq = ao.als(W, fs, 1, MAX_ITER, eps=0.0)
     run = LayerRun("layer1.0.conv1", _t(torch, dev, W), R, [_t(torch, dev, f) for f in fs])
     iters = als_sweep([run], MAX_ITER, 0.0, 4, MSE)
     assert iters[id(run)] == 3 * (MAX_ITER - 1)
     for f, q in zip(run.factors, run.quantized):
         _levels(f.cpu().numpy())
         _levels(q.cpu().numpy())
-    print(f"C2 sweep: rec_error gpu {run.loss[-1]:.6f} oracle {loss[-1]:.6f}; "
-          f"quant_rec_error gpu {run.lossq[-1]:.6f} oracle {lossq[-1]:.6f}")
-    assert abs(run.loss[-1] - loss[-1]) / loss[-1] < 0.02
-    assert abs(run.lossq[-1] - lossq[-1]) / lossq[-1] < 0.02
+    print(f"C2 sweep: rec_error gpu {run.loss[-1]:.6f}, reference {min(ref['rec_error']):.6f} .. "
+          f"{max(ref['rec_error']):.6f}; quant_rec_error gpu {run.lossq[-1]:.6f}, reference "
+          f"{min(ref['quant_rec_error']):.6f} .. {max(ref['quant_rec_error']):.6f}")
+    lo, hi = _band(ref["rec_error"])
+    assert lo <= run.loss[-1] <= hi, (run.loss[-1], lo, hi)
+    lo, hi = _band(ref["quant_rec_error"])
+    assert lo <= run.lossq[-1] <= hi, (run.lossq[-1], lo, hi)
 
 
 def test_c3_batch_at_bench_horizon(torch_dev):

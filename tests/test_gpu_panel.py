@@ -88,12 +88,13 @@ def test_tile_count_grows_on_one_workspace(env):
     Xd = X.double()
     lib = __import__("admmq")._lib.load()
     ws = torch.zeros(lib.admmq_panel_workspace_size(2048, 2048, 256), dtype=torch.uint8, device=dev)
-    panel._WS[X.device] = ws   # one workspace for every call below
+    key = panel._key(X.device)   # (device, current stream): the workspace these calls use
+    panel._WS[key] = ws          # one workspace for every call below
     for k in (32, 256, 64, 256, 32, 160):
         Q = torch.randn(2048, k, generator=g, dtype=torch.float64).to(dev)
         assert _colrel(panel.xtq(X, Q), Xd.T @ Q) < 1e-13
         assert _colrel(panel.xy(X, Q), Xd @ Q) < 1e-13
-    assert panel._WS[X.device] is ws
+    assert panel._WS[key] is ws
 
 
 @pytest.mark.parametrize("m,n,r", [(4096, 4096, 8), (1000, 777, 32), (17, 5, 3)])

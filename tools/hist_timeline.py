@@ -19,6 +19,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--shapes", default="", help="I:R,I:R,... instead of the resnet18 factors of --mode")
+ap.add_argument("--spread", type=int, default=-1, help="admmq_debug_set_search_spread (default: library's)")
+ap.add_argument("--pl", type=int, default=-1, help="admmq_debug_set_search_pl (default: library's)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 g = torch.Generator().manual_seed(0)
@@ -32,6 +34,10 @@ for I, R in shapes:
     H = torch.randn(I, R, generator=g).to(dev) * 0.1
     U = torch.zeros(I, R, device=dev)
     probs.append((H, U, F, G))
+if a.spread >= 0:
+    _lib.load().admmq_debug_set_search_spread(a.spread)
+if a.pl >= 0:
+    _lib.load().admmq_debug_set_search_pl(a.pl)
 admm_iteration_batched(probs, a.iters, 0.0, 4, "tensor_mseminmax_symmetric", check_spd=False)
 torch.cuda.synchronize()
 lib = _lib.load()
@@ -66,8 +72,14 @@ if fused and hasattr(lib, "admmq_debug_fin_trace"):
     fr = [(f, r) for f, r in fr if f[0] >= r[4] and f[3] >= f[0]]
     if fr:
         print(f"  finalize sub-phases over {len(fr)} blocks:")
-        for name, a0, a1 in (("start->rho", None, 0), ("rho->loads done", 0, 4), ("elements+stores", 4, 1),
-                             ("rowmax barrier", 1, 2), ("split stores", 2, 3), ("residuals+end", 3, None)):
+        # stamps 2 / 3 (row-max barrier, split stores) exist only in the split solve form;
+        # elsewhere column 2 holds a stale value of an earlier launch, so the phases between
+        # stamp 1 and the end are reported as one
+        split = all(f[1] <= f[2] <= f[3] for f, _ in fr)
+        sub = [("start->rho", None, 0), ("rho->loads done", 0, 4), ("elements+stores", 4, 1)]
+        sub += ([("rowmax barrier", 1, 2), ("split stores", 2, 3), ("residuals+end", 3, None)] if split
+                else [("residuals+end", 1, None)])
+        for name, a0, a1 in sub:
             d = [((f[a1] if a1 is not None else r[5]) - (f[a0] if a0 is not None else r[4])) / 100 for f, r in fr]
             print(f"    {name:16s} avg {sum(d)/len(d):6.2f}  max {max(d):6.2f} us")
 sfn = getattr(lib, "admmq_debug_setup_trace", None)
@@ -81,10 +93,20 @@ if sfn is not None:
         for k, nm in enumerate(["thresholds+scatter", "ties", "check+L+cells", "(fallback)"]):
             d = [(r[k + 1] - r[k]) / 100 for r in sr]
             print(f"    {nm:18s} avg {sum(d) / len(d):6.2f}  max {max(d):6.2f} us")
-cus = {}
-for r in rows:
-    cus.setdefault(r[5], []).append(r)
-print(f"  CUs used {len(cus)}; blocks per CU max {max(len(v) for v in cus.values())}")
+# the CU of each block: (XCC_ID << 32) | HW_ID from admmq_debug_hist_cu (column 5 of the
+# fused kernel's trace is a time stamp, not a CU id); key (XCC, SE, SH, CU) as gemm_timeline.py
+cfn = getattr(lib, "admmq_debug_hist_cu", None)
+if cfn is not None:
+    cb = (ctypes.c_ulonglong * n)()
+    cfn(cb, n)
+    cus = {}
+    for b in range(len(rows)):
+        hid = cb[b]
+        hw = hid & 0xFFFFFFFF
+        cus.setdefault(((hid >> 32) & 0xFF, (hw >> 13) & 0x7, (hw >> 12) & 1, (hw >> 8) & 0xF), []).append(b)
+    per = sorted(len(v) for v in cus.values())
+    print(f"  CUs used {len(cus)}; blocks per CU max {per[-1]}; CUs with 1 / 2 / >2 blocks: "
+          f"{per.count(1)} / {per.count(2)} / {sum(1 for x in per if x > 2)}")
 
 pb = (ctypes.c_ulonglong * (5 * 256))()
 gp = lib.admmq_debug_prep_trace(pb, 256) if hasattr(lib, "admmq_debug_prep_trace") else 0

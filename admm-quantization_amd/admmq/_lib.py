@@ -113,9 +113,9 @@ def load() -> ctypes.CDLL:
         "admmq_debug_ksplit_balance_count": (ctypes.c_int64, [ctypes.c_void_p, I32]),
         "admmq_debug_ksplit_pieces": (I32, [I32, I32]),
         "admmq_debug_set_even_units": (I32, [I32]),
-        "admmq_debug_set_search_spread": (I32, [I32]),
-        "admmq_debug_set_search_pl": (I32, [I32]),
         "admmq_spd_solve64": (I32, [P, P, I64, I64, P, P, P]),
+        "admmq_debug_epc_evals": (I32, [P, I32]),
+        "admmq_debug_spd_trace": (I32, [P]),
         "admmq_epc_step64": (I32, [P, P, I64, I64, ctypes.c_double, ctypes.c_double, P, P, P, P]),
         "admmq_debug_hist_cu": (I32, [P, I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
@@ -296,27 +296,6 @@ class fin_nv3:
 
     def __exit__(self, *exc):
         load().admmq_debug_set_fin_nv3(1)
-        return False
-
-
-class search_form:
-    """Context manager (diagnostics): the big jobs' stage-1 form, ``pl`` 0 = merged
-    thresholds, 1 = per level where a launch has at most one block per CU (default), 2 = per
-    level wherever the plan allows; ``spread`` 1 = a launch of at most one block per CU takes
-    one CU per block (default), 0 = the dispatcher's placement. Same integers, same bits.
-    Restores the defaults on exit."""
-
-    def __init__(self, pl: int = 1, spread: int = 1):
-        self.pl, self.spread = pl, spread
-
-    def __enter__(self):
-        check(load().admmq_debug_set_search_pl(self.pl), "search_pl")
-        check(load().admmq_debug_set_search_spread(self.spread), "search_spread")
-        return self
-
-    def __exit__(self, *exc):
-        load().admmq_debug_set_search_pl(1)
-        load().admmq_debug_set_search_spread(1)
         return False
 
 

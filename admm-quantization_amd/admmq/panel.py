@@ -135,7 +135,7 @@ def epc_mu(c: torch.Tensor, s: torch.Tensor, normY2: float, delta2: float) -> to
     return mu
 
 
-SPD_SMALL_MAX = 140   # n of the one-workgroup fp64 solves (csrc/epc_kernels.hip: the matrix in LDS)
+SPD_SMALL_MAX = 136   # n of the one-workgroup fp64 solves (csrc/epc_kernels.hip: the matrix in LDS)
 
 
 def spd_solve64(G: torch.Tensor, F: torch.Tensor) -> torch.Tensor:

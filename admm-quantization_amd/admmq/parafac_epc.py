@@ -24,7 +24,7 @@ CP identity ||Y||^2 - 2 <Y, [[w; U]]> + ||[[w; U]]||^2 on those products (no I x
 reconstruction, as tensorly's ``parafac`` does); the R x R solves run on one workgroup with
 the matrix in LDS (``panel.spd_solve64`` for the CP-ALS update, ``panel.epc_step64`` for the
 EPC update: Cholesky factors of G + mu I and Newton steps on the error equation instead of
-an eigendecomposition; ``csrc/epc_kernels.hip``) for R <= 140, torch linear algebra above
+an eigendecomposition; ``csrc/epc_kernels.hip``) for R <= 136, torch linear algebra above
 that. The stopping scalars stay on the device: the drivers run ``_CHECK_EVERY`` iterations
 between host reads, keep each iteration's factors, and on a stop return those of the
 iteration the reference would have stopped at (the same iterations and results as a

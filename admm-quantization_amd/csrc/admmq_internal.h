@@ -257,14 +257,11 @@ int check_cells(int n, int bits, unsigned seed, int nsamp, unsigned* maxdev_out)
 bool merged_ok(int ncand, int bits);
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-                      size_t lds_floor = 0, bool pl = false);
-bool histl_ok(int ncand, int bits);
-size_t histl_lds_bytes(int ncand, int bits);
+                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // fused finalize: polls (s_sleep 2 each, ~10 ms in all) before a block gives up waiting for
 // its job's selection and reports an internal fault instead of finalizing
 constexpr unsigned kFinWaitPollsDefault = 1u << 17;
-int hist3_fin_capacity(int ncand, int bits, int nv, bool pl = false);
+int hist3_fin_capacity(int ncand, int bits, int nv);
 int small_admm_groups(long long maxtotal);
 void launch_mse_small_admm(const ProbDesc* d, const int* jobs, int njobs, int ngr, int ncand, int bits, int slot,
                            int iter, const unsigned short* rank0, const unsigned short* groups, int ngroups,

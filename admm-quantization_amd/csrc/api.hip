@@ -160,16 +160,7 @@ static std::atomic<int> g_f32_rule{1};
 // fp32 solve kernel: 0 = k_gemm (64 x 64 tiles), 1 = persistent tile lists (k_gemm_f32p,
 // slower: DESIGN §7), 2 = one tile per workgroup with per-problem tile rows (k_gemm_f32t)
 static std::atomic<int> g_f32_kernel{0};
-static std::atomic<int> g_even_units{1};
-// a search launch of at most one block per CU asks for 96 KB of LDS per block (one block
-// per CU): its blocks are spread over the CUs instead of stacked (diagnostic switch)
-static std::atomic<int> g_search_spread{1};
-static constexpr size_t kSpreadLds = 96 * 1024;
-// stage-1 form of the big jobs' search: 0 = merged thresholds (k_mse_hist3), 2 = per level
-// (k_mse_hist3<.., PL>), 1 = per level where a launch has at most one block per CU (its
-// blocks hold few elements per thread: the table and flush it saves weigh more than its
-// dearer inserts)
-static std::atomic<int> g_search_pl{1};   // big-job stage-1 units sized to fill the resident round evenly
+static std::atomic<int> g_even_units{1};   // big-job stage-1 units sized to fill the resident round evenly
 static int f32_tile_rows(int I, int ld) {
   if (I <= 32) return 32;
   const int rule = g_f32_rule.load();
@@ -1323,19 +1314,6 @@ int32_t admmq_debug_set_even_units(int32_t on) {
   g_even_units = on != 0;
   return ADMMQ_OK;
 }
-// diagnostics: 0 = search launches of at most one block per CU take their own LDS size
-// (the dispatcher may stack them), 1 = the 96 KB floor that spreads them (default)
-int32_t admmq_debug_set_search_spread(int32_t on) {
-  g_search_spread = on != 0;
-  return ADMMQ_OK;
-}
-// diagnostics: stage-1 form of the big jobs' search, 0 = merged, 1 = per level where a
-// launch has at most one block per CU (default), 2 = per level always (same bits)
-int32_t admmq_debug_set_search_pl(int32_t v) {
-  if (v < 0 || v > 2) return fail(ADMMQ_ERR_ARG, "search_pl must be 0..2");
-  g_search_pl = v;
-  return ADMMQ_OK;
-}
 
 int32_t admmq_debug_set_gemm_stage(int32_t v) {
   if (v < 0 || v > 4) return fail(ADMMQ_ERR_ARG, "stage must be 0..4");
@@ -1563,15 +1541,8 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
   const bool fused_allowed = opt->fused_finalize != 0 && info != nullptr;
   const bool fin_ok = fused_allowed && qscheme == kMse && !exhaustive && merged && pl.rows_aligned && nh_big > 0;
   const int cap_over = g_fin_cap_override.load();
-  // the per-level stage 1 where the launch has at most one block per CU (g_search_pl)
-  const int nh_launch = fin_ok ? nh_big : (fuse_small ? pl.nhm_big : (int)pl.hist_multi.size());
-  // (one float4 pair per thread: the per-level inserts of two pairs held across the fused
-  // finalize's wait spill 25 VGPRs)
-  const bool search_pl = merged && histl_ok(num_attempts, bits) && pl.hist_nv == 1 &&
-                         (g_search_pl.load() == 2 || (g_search_pl.load() == 1 && nh_launch <= device_cus()));
-  const int fin_cap = fin_ok ? (cap_over > 0 ? std::min(cap_over, hist3_fin_capacity(num_attempts, bits, pl.hist_nv,
-                                                                                     search_pl))
-                                             : hist3_fin_capacity(num_attempts, bits, pl.hist_nv, search_pl))
+  const int fin_cap = fin_ok ? (cap_over > 0 ? std::min(cap_over, hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
+                                             : hist3_fin_capacity(num_attempts, bits, pl.hist_nv))
                              : 0;
   // one whole-row unit per block, all blocks resident; a launch with more units than that
   // takes the separate finalize launch (round 3 measured blocks taking several units each
@@ -1628,11 +1599,9 @@ int32_t admmq_admm_run_ex(const admmq_problem* probs, int32_t nprob, int32_t max
         if (nh > 0) {
           hipEvent_t h0, h1;
           prof_pair(ADMMQ_PROF_SEARCH, &h0, &h1);
-          const size_t lds_floor = (g_search_spread.load() && nh <= device_cus()) ? kSpreadLds : 0;
           launch_mse_hist3(pl.d_desc, nullptr,
                            fuse_fin ? pl.d_hist : pl.d_hist_multi, nh, num_attempts,
-                           bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s, h0, h1,
-                           lds_floor, search_pl);
+                           bits, slot, pl.d_rank0, pl.d_groups, ngroups, pl.hist_nv, fuse_fin, it, polls, s, h0, h1);
         }
         if (fuse_small) {   // the small jobs' search and finalize in one block each
           prof_class(ADMMQ_PROF_SMALL); prof_mark(s);

@@ -875,17 +875,6 @@ __device__ __forceinline__ void h3_totals(int c, int n, const unsigned short* rn
   t2 += (unsigned long long)(2 * QMAX - 1) * cntN[L];
 }
 
-// Dynamic LDS of the per-level form (PL): thresholds [QMAX][n], bins h1 (n + 65 u64: 1..n,
-// then one private dummy per lane), h2 (n + 65 u32); the last block's suffix arrays and
-// stage-2 tiles reuse it
-__host__ __device__ inline size_t histl_off_h1(int n, int qmax) { return ((size_t)qmax * n * 4 + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t histl_off_h2(int n, int qmax) { return histl_off_h1(n, qmax) + (size_t)(n + 65) * 8; }
-size_t histl_lds_bytes(int ncand, int bits) {
-  const int qmax = 1 << (bits - 1);
-  const size_t b = (histl_off_h2(ncand, qmax) + (size_t)(ncand + 65) * 4 + 15) & ~(size_t)15;
-  return std::max(std::max(b, (size_t)2 * kH3Threads * 8), (size_t)kSseQuads * 16);
-}
-
 // FIN (ADMM jobs only): the search launch also runs the finalize step (k_finalize_admm's
 // projection + dual update + next right-hand side) on the block's own elements, which
 // it already holds: units are whole rows, every block of the launch is resident at once
@@ -906,17 +895,7 @@ constexpr bool kFinStream = ADMMQ_FIN_STREAM != 0;   // the fused finalize store
 // NV = 3 (FIN: the launches whose units would not all be resident at 2 groups per thread,
 // e.g. C4): U is re-read with H and F for the finalize instead of held across the search
 // (its registers are what would spill), an L2 hit written by the solve's epilogue.
-//
-// PL (per-level stage 1, hist_insert_elem as in the thin loop): the table is the QMAX x n
-// thresholds themselves (one pass, no host order, ties or cell index), each element finds
-// its breakpoint per level from a linear estimate and two neighbouring thresholds, and the
-// block's bins are per candidate (b = #candidates reached at a level), so the flush needs
-// no bucket scan: the last block forms T(c) = sum_{b > c} bin[b] by one suffix scan over
-// the n + 1 bins. The same integers T1(c), T2(c) as the merged form (every (element,
-// level) pair with a >= thr[k][c] adds af and 2k - 1 once), hence the same selection and
-// bits. Cheaper setup and flush, dearer inserts: the host takes it where a block holds few
-// elements per thread (a lone layer, the small shards of a multi-GPU run).
-template <int QMAX, int NV, bool FIN, bool PL = false>
+template <int QMAX, int NV, bool FIN>
 __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     const ProbDesc* __restrict__ d, const QJob* __restrict__ qj, const Chunk* __restrict__ chunks, int ncand, int slot,
     const unsigned short* __restrict__ rank0, const unsigned short* __restrict__ groups, int ngroups, int bits,
@@ -930,7 +909,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   const float mx = __uint_as_float(gld_u32(ck.stat + 4 * slot));
   const long long total = ck.total;
   H3Pre pre;
-  if constexpr (!PL) h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kH3Threads);
+  h3_load_order(rank0, QMAX * ncand, groups, ngroups, pre, kH3Threads);
   asm volatile("" ::: "memory");   // issue order: the loads above before the element loads
   constexpr bool kReloadU = FIN && NV >= 3;
   float4 x4[2 * NV], u4[2 * NV], h4[FIN ? 2 * NV : 1], f4[FIN ? 2 * NV : 1];
@@ -985,190 +964,105 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     }
     return;
   }
-  unsigned long long tstamp[3] = {T0, 0ull, 0ull};   // {start, table ready, elements done}
-  if constexpr (PL) {
-    // the QMAX x n thresholds: thread (candidate c, half of the levels) computes s_c once
-    float* thr = reinterpret_cast<float*>(smem);                                        // [QMAX][n]
-    unsigned long long* pb1 = reinterpret_cast<unsigned long long*>(smem + histl_off_h1(n, QMAX));   // n + 65
-    unsigned* pb2 = reinterpret_cast<unsigned*>(smem + histl_off_h2(n, QMAX));                        // n + 65
-    {
-      constexpr int KH = (QMAX + 1) / 2;
-      const float den = (float)(2 * QMAX - 1);
-      for (int e = threadIdx.x; e < 2 * n; e += kH3Threads) {
-        const int c = e >> 1, k0 = 1 + (e & 1) * KH;
-        const float sc = (2.0f * cand_t(mx, c, n)) / den;
-#pragma unroll
-        for (int k = k0; k < k0 + KH; ++k)
-          if (k <= QMAX) thr[(k - 1) * n + c] = level_threshold_fast(sc, k);
-      }
-    }
-    for (int b = threadIdx.x; b < n + 65; b += kH3Threads) { pb1[b] = 0ull; pb2[b] = 0u; }
-    __syncthreads();
-    const unsigned long long T1 = ADMMQ_NOW();
-    const float S0 = (float)(0.2 * (double)mx);
-    const float E0 = (float)(1.2 * (double)mx);
-    const float inv_step = (float)(n - 1) / (E0 - S0);
-    const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
-    float tlo0[QMAX], thin[QMAX];   // per level: thresholds of the first and the last candidate
-#pragma unroll
-    for (int k = 0; k < QMAX; ++k) { tlo0[k] = thr[k * n]; thin[k] = thr[k * n + n - 1]; }
-    double s2 = 0.0;
-    unsigned long long full1 = 0ull;
-    unsigned full2 = 0u;
-    const int reps = FIN ? 1 : max(ck.reps, 1);
+  const int M = QMAX * n;
+  const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
+  unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
+  unsigned long long* sumN = sumA + nb;
+  unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
+  unsigned* cntN = cntA + nb;
+  float* thr = reinterpret_cast<float*>(cntN + nb);                          // M
+  float* tsort = thr + M;                                                    // M
+  unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
+  unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
+  const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, rank0 + kMaxMerged, sumA, sumN, cntA, cntN, thr, tsort,
+                                   rnk, cell, kH3Threads);
+  const unsigned long long T1 = ADMMQ_NOW();
+  const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
+  const int dummy = M + 1 + (threadIdx.x & 63);
+  double s2 = 0.0;
+  // a block may take several consecutive units of its job (ck.reps, `step` elements each):
+  // one table setup and one flush for all of them (not FIN: the fused finalize's launch
+  // has one unit per block, all resident)
+  const int reps = FIN ? 1 : max(ck.reps, 1);
+  if constexpr (!FIN) {
+    // several units per block: X - U of unit r is formed first (its x4 / u4 registers are
+    // then free), the loads of unit r + 1 are issued into them, and unit r's inserts run
+    // while those loads are in flight (the same elements, sums and order as one unit at a
+    // time; 16 NV more VGPRs, not 32 NV)
     for (int r = 0; r < reps; ++r) {
       const long long ub = (long long)ck.start + (long long)r * ck.step;
       const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
-      if (r > 0) {   // this unit's elements (unit 0's were issued before the table)
-#pragma unroll
-        for (int hh = 0; hh < 2 * NV; ++hh) {
-          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-          x4[hh] = gld4(ck.X + (e < ue ? e : 0));
-          if (ck.U) u4[hh] = gld4(ck.U + (e < ue ? e : 0));
-        }
-      }
+      float4 xv[2 * NV];
 #pragma unroll
       for (int hh = 0; hh < 2 * NV; ++hh) {   // X - U (ADMM: H_T - U); zero past the end
         float4 xa = x4[hh];
         if (ck.U) xa = sub4(xa, u4[hh]);
         const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-        if (e >= ue) xa = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float xs[4] = {xa.x, xa.y, xa.z, xa.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)   // (sums x^2 into s2 itself)
-          hist_insert_elem<QMAX>(xs[j], thr, n, S0, inv_step, K1, 0, tlo0, thin, pb1, pb2, s2, full1, full2);
+        xv[hh] = e >= ue ? make_float4(0.f, 0.f, 0.f, 0.f) : xa;
       }
-    }
+      if (r + 1 < reps) {
+        const long long nb = ub + ck.step, ne = min(nb + ck.step, total);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      full1 += __shfl_xor(full1, off);
-      full2 += (unsigned)__shfl_xor((int)full2, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      if (full1) atomicAdd(&pb1[n], full1);
-      if (full2) atomicAdd(&pb2[n], full2);
-    }
-    __syncthreads();
-    const unsigned long long T2 = ADMMQ_NOW();
-    // the block's bins 1..n into one of kHistRep replicas of the job's bins
-    const int rep = blockIdx.x & (kHistRep - 1);
-    unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
-    unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
-    for (int b = 1 + threadIdx.x; b <= n; b += kH3Threads) {
-      if (pb1[b]) atomicAdd(&g1[b], pb1[b]);
-      if (pb2[b]) atomicAdd(&g2[b], (unsigned long long)pb2[b]);
-    }
-    s2 = wave_sum_f64(s2);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int w = 0; w < kH3Threads / 64; ++w) t += red[w];
-      atomicAdd(&v.s2[slot], t);
-    }
-    tstamp[1] = T1; tstamp[2] = T2;
-  } else {
-    const int M = QMAX * n;
-    const int nb = M + 1 + 64;                  // buckets 0..M, then one private dummy per lane
-    unsigned long long* sumA = reinterpret_cast<unsigned long long*>(smem);   // positives, then all
-    unsigned long long* sumN = sumA + nb;
-    unsigned* cntA = reinterpret_cast<unsigned*>(sumN + nb);
-    unsigned* cntN = cntA + nb;
-    float* thr = reinterpret_cast<float*>(cntN + nb);                          // M
-    float* tsort = thr + M;                                                    // M
-    unsigned short* rnk = reinterpret_cast<unsigned short*>(tsort + M);        // M: rank, then L
-    unsigned short* cell = rnk + ((M + 1) & ~1);                               // kCells + 1
-    const float inv = h3_setup<QMAX>(mx, n, pre, groups, ngroups, rank0 + kMaxMerged, sumA, sumN, cntA, cntN, thr, tsort,
-                                     rnk, cell, kH3Threads);
-    const unsigned long long T1 = ADMMQ_NOW();
-    const int K1 = hist_fixed_exp(mx, v.nelem, QMAX);
-    const int dummy = M + 1 + (threadIdx.x & 63);
-    double s2 = 0.0;
-    // a block may take several consecutive units of its job (ck.reps, `step` elements each):
-    // one table setup and one flush for all of them (not FIN: the fused finalize's launch
-    // has one unit per block, all resident)
-    const int reps = FIN ? 1 : max(ck.reps, 1);
-    if constexpr (!FIN) {
-      // several units per block: X - U of unit r is formed first (its x4 / u4 registers are
-      // then free), the loads of unit r + 1 are issued into them, and unit r's inserts run
-      // while those loads are in flight (the same elements, sums and order as one unit at a
-      // time; 16 NV more VGPRs, not 32 NV)
-      for (int r = 0; r < reps; ++r) {
-        const long long ub = (long long)ck.start + (long long)r * ck.step;
-        const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
-        float4 xv[2 * NV];
-  #pragma unroll
-        for (int hh = 0; hh < 2 * NV; ++hh) {   // X - U (ADMM: H_T - U); zero past the end
-          float4 xa = x4[hh];
-          if (ck.U) xa = sub4(xa, u4[hh]);
-          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-          xv[hh] = e >= ue ? make_float4(0.f, 0.f, 0.f, 0.f) : xa;
-        }
-        if (r + 1 < reps) {
-          const long long nb = ub + ck.step, ne = min(nb + ck.step, total);
-  #pragma unroll
-          for (int hh = 0; hh < 2 * NV; ++hh) {
-            const long long e = nb + 4LL * threadIdx.x + 2048LL * hh;
-            x4[hh] = gld4(ck.X + (e < ne ? e : 0));
-            if (ck.U) u4[hh] = gld4(ck.U + (e < ne ? e : 0));
-          }
-        }
-  #pragma unroll
-        for (int hb = 0; hb < 2 * NV; hb += 2) {
-          const float4 xa = xv[hb], xb = xv[hb + 1];
-          const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-  #pragma unroll
-          for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
-          h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
-        }
-      }
-    }
-    for (int r = 0; FIN && r < reps; ++r) {
-      const long long ub = (long long)ck.start + (long long)r * ck.step;   // unit r (r > 0: reps > 1 only)
-      const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
-      if (r > 0) {   // this unit's elements (unit 0's were issued before the table setup)
-  #pragma unroll
         for (int hh = 0; hh < 2 * NV; ++hh) {
-          const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
-          x4[hh] = gld4(ck.X + (e < ue ? e : 0));
-          if (ck.U) u4[hh] = gld4(ck.U + (e < ue ? e : 0));
+          const long long e = nb + 4LL * threadIdx.x + 2048LL * hh;
+          x4[hh] = gld4(ck.X + (e < ne ? e : 0));
+          if (ck.U) u4[hh] = gld4(ck.U + (e < ne ? e : 0));
         }
       }
-  #pragma unroll
-      for (int hb = 0; hb < 2 * NV; hb += 2) {   // X - U (ADMM: H_T - U); zero past the end
-        float4 xa = x4[hb], xb = x4[hb + 1];
-        if (ck.U) { xa = sub4(xa, u4[hb]); xb = sub4(xb, u4[hb + 1]); }
-        const long long e = ub + 4LL * threadIdx.x + 2048LL * hb;
-        if (e >= ue) xa = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e + 2048 >= ue) xb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int hb = 0; hb < 2 * NV; hb += 2) {
+        const float4 xa = xv[hb], xb = xv[hb + 1];
         const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-  #pragma unroll
+#pragma unroll
         for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
         h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
       }
     }
-    __syncthreads();
-    const unsigned long long T2 = ADMMQ_NOW();
-    h3_suffix<kH3Threads, 4>(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
-    // per-candidate totals of this block into one of kHistRep replicas
-    const int rep = blockIdx.x & (kHistRep - 1);
-    unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
-    unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
-    for (int c = threadIdx.x; c < n; c += blockDim.x) {
-      unsigned long long t1, t2;
-      h3_totals<QMAX>(c, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
-      if (t1) atomicAdd(&g1[c], t1);
-      if (t2) atomicAdd(&g2[c], t2);
+  }
+  for (int r = 0; FIN && r < reps; ++r) {
+    const long long ub = (long long)ck.start + (long long)r * ck.step;   // unit r (r > 0: reps > 1 only)
+    const long long ue = reps > 1 ? min(ub + ck.step, total) : total;
+    if (r > 0) {   // this unit's elements (unit 0's were issued before the table setup)
+#pragma unroll
+      for (int hh = 0; hh < 2 * NV; ++hh) {
+        const long long e = ub + 4LL * threadIdx.x + 2048LL * hh;
+        x4[hh] = gld4(ck.X + (e < ue ? e : 0));
+        if (ck.U) u4[hh] = gld4(ck.U + (e < ue ? e : 0));
+      }
     }
-    s2 = wave_sum_f64(s2);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-      atomicAdd(&v.s2[slot], t);
+#pragma unroll
+    for (int hb = 0; hb < 2 * NV; hb += 2) {   // X - U (ADMM: H_T - U); zero past the end
+      float4 xa = x4[hb], xb = x4[hb + 1];
+      if (ck.U) { xa = sub4(xa, u4[hb]); xb = sub4(xb, u4[hb + 1]); }
+      const long long e = ub + 4LL * threadIdx.x + 2048LL * hb;
+      if (e >= ue) xa = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e + 2048 >= ue) xb = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2 += (double)xs[j] * (double)xs[j];
+      h3_insert_n<8>(xs, inv, tsort, cell, M, K1, dummy, sumA, sumN, cntA, cntN);
     }
-    tstamp[1] = T1; tstamp[2] = T2;
+  }
+  __syncthreads();
+  const unsigned long long T2 = ADMMQ_NOW();
+  h3_suffix<kH3Threads, 4>(M, sumA, sumN, cntA, cntN, wtot, wtot2, wtot32, wtot32b);
+  // per-candidate totals of this block into one of kHistRep replicas
+  const int rep = blockIdx.x & (kHistRep - 1);
+  unsigned long long* g1 = v.h1 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  unsigned long long* g2 = v.h2 + ((size_t)slot * kHistRep + rep) * (n + 1);
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    unsigned long long t1, t2;
+    h3_totals<QMAX>(c, n, rnk, sumA, sumN, cntA, cntN, t1, t2);
+    if (t1) atomicAdd(&g1[c], t1);
+    if (t2) atomicAdd(&g2[c], t2);
+  }
+  s2 = wave_sum_f64(s2);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    atomicAdd(&v.s2[slot], t);
   }
   // ticket: the last block of this job selects the candidate set (all its inputs were
   // written by device-scope atomics: drain them, no L2 writeback needed)
@@ -1181,8 +1075,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
   const unsigned long long T3 = ADMMQ_NOW();
   auto trace = [&](unsigned long long T4) {
     if (ADMMQ_TRACE && threadIdx.x == 0 && blockIdx.x < kHistTraceMax) {
-      g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = tstamp[1];
-      g_hist_trace[blockIdx.x][2] = tstamp[2];
+      g_hist_trace[blockIdx.x][0] = T0; g_hist_trace[blockIdx.x][1] = T1; g_hist_trace[blockIdx.x][2] = T2;
       g_hist_trace[blockIdx.x][3] = T3; g_hist_trace[blockIdx.x][4] = T4; g_hist_trace[blockIdx.x][5] = 0;
       g_hist_cu[blockIdx.x] = ((unsigned long long)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFF) << 32) |
                               __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -1199,33 +1092,7 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
     // (a one-wave form - lane l summing candidates 4l .. 4l + 3 over the kHistRep replicas
     // itself - made the other blocks' wait for this selection 8.0 -> 16.8 us at C3: 64
     // dependent sc1 loads per lane against 16 per thread here)
-    if constexpr (PL) {
-      // bins b = 1..n summed over the replicas (thread b), then T(c) = sum_{b > c} bin[b]:
-      // an inclusive block suffix scan over b (n + 2 <= the block; the host checks)
-      unsigned long long* suf1 = reinterpret_cast<unsigned long long*>(smem);   // [kH3Threads] each
-      unsigned long long* suf2 = suf1 + kH3Threads;
-      const int b = threadIdx.x, lane = b & 63, w = b >> 6;
-      unsigned long long t1 = 0ull, t2 = 0ull;
-      if (b >= 1 && b <= n) {
-#pragma unroll
-        for (int r = 0; r < kHistRep; ++r) {
-          t1 += __hip_atomic_load((gu64*)&G1[r * (n + 1) + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          t2 += __hip_atomic_load((gu64*)&G2[r * (n + 1) + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      unsigned long long q1 = wave_suffix_u64(t1), q2 = wave_suffix_u64(t2);
-      if (lane == 0) { wtot[w] = q1; wtot2[w] = q2; }
-      __syncthreads();
-#pragma unroll
-      for (int j = 1; j < kH3Threads / 64; ++j)
-        if (j > w) { q1 += wtot[j]; q2 += wtot2[j]; }
-      suf1[b] = q1; suf2[b] = q2;
-      __syncthreads();
-      const double S2 = __hip_atomic_load((__attribute__((address_space(1))) double*)&v.s2[slot], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-      const int c = threadIdx.x;
-      select_block(v, sel, lsel, c < n ? suf1[c + 1] : 0ull, c < n ? suf2[c + 1] : 0ull, S2, mx, n, QMAX);
-    } else if (n <= (int)blockDim.x) {
+    if (n <= (int)blockDim.x) {
       const int c = threadIdx.x;
       unsigned long long t1 = 0ull, t2 = 0ull;
       if (c < n) {
@@ -1239,8 +1106,8 @@ __global__ __launch_bounds__(kH3Threads, 4) void k_mse_hist3(
                                           __HIP_MEMORY_SCOPE_AGENT);
       select_block(v, sel, lsel, t1, t2, S2, mx, n, QMAX);
     } else {
-      unsigned long long* T1v = reinterpret_cast<unsigned long long*>(smem);   // reuse LDS: n each
-      unsigned long long* T2v = T1v + n;
+      unsigned long long* T1v = sumA;                 // reuse LDS: n each
+      unsigned long long* T2v = sumN;
       for (int c = threadIdx.x; c < n; c += blockDim.x) {
         unsigned long long t1 = 0ull, t2 = 0ull;
 #pragma unroll
@@ -1580,51 +1447,31 @@ void launch_mse_hist(const ProbDesc* d, const QJob* q, const Chunk* chunks, int 
 bool merged_ok(int ncand, int bits) {
   return ncand >= 2 && ((size_t)ncand << (bits - 1)) <= (size_t)kMaxMerged && hist3_lds_bytes(ncand, bits) <= 150 * 1024;
 }
-// The per-level form (PL) where the launch holds few elements per block thread: bits 2..4,
-// ncand <= kTLMaxCand (the last block's suffix scan takes one bin per thread)
-bool histl_ok(int ncand, int bits) { return bits >= 2 && bits <= 4 && ncand >= 2 && ncand <= kTLMaxCand; }
 void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int nchunks, int ncand, int bits, int slot,
                       const unsigned short* rank0, const unsigned short* groups, int ngroups, int nv, bool fin, int iter,
-                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, size_t lds_floor, bool pl) {
+                      unsigned wait_polls, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   if (nchunks <= 0) return;
-  pl = pl && histl_ok(ncand, bits);
-  // lds_floor: a launch of at most one block per CU asks for more LDS than two blocks can
-  // hold, so the dispatcher cannot stack its blocks on a few CUs (their setup, inserts and
-  // flush would then share one CU's LDS and VALU while other CUs idle)
-  const size_t lds = std::max(pl ? histl_lds_bytes(ncand, bits) : hist3_lds_bytes(ncand, bits), lds_floor);
+  const size_t lds = hist3_lds_bytes(ncand, bits);
   // ev0 / ev1 (profiling, may be null): recorded by the dispatch itself at the kernel's start / end
-#define ADMMQ_H3(Q, V, F, L)                                                                                       \
-  do {                                                                                                             \
-    if (lds > 64 * 1024)                                                                                           \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_mse_hist3<Q, V, F, L>),                            \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
-    hipExtLaunchKernelGGL((k_mse_hist3<Q, V, F, L>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q,  \
-                          chunks, ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls);                    \
-  } while (0)
-#define ADMMQ_H3N(Q, L)                            \
+#define ADMMQ_H3(Q, V, F)                                                                                         \
+  hipExtLaunchKernelGGL((k_mse_hist3<Q, V, F>), dim3(nchunks), dim3(kH3Threads), lds, s, ev0, ev1, 0u, d, q, chunks, \
+                        ncand, slot, rank0, groups, ngroups, bits, iter, wait_polls)
+#define ADMMQ_H3N(Q)                               \
   if (fin) {                                       \
-    if (nv == 3) ADMMQ_H3(Q, 3, true, L);          \
-    else if (nv == 2) ADMMQ_H3(Q, 2, true, L);     \
-    else ADMMQ_H3(Q, 1, true, L);                  \
+    if (nv == 3) ADMMQ_H3(Q, 3, true);             \
+    else if (nv == 2) ADMMQ_H3(Q, 2, true);        \
+    else ADMMQ_H3(Q, 1, true);                     \
   } else {                                         \
-    if (nv == 3) ADMMQ_H3(Q, 3, false, L);         \
-    else if (nv == 2) ADMMQ_H3(Q, 2, false, L);    \
-    else ADMMQ_H3(Q, 1, false, L);                 \
-  }
-  if (pl) {
-    switch (bits) {
-      case 2: ADMMQ_H3N(2, true); break;
-      case 3: ADMMQ_H3N(4, true); break;
-      default: ADMMQ_H3N(8, true); break;
-    }
-    return;
+    if (nv == 3) ADMMQ_H3(Q, 3, false);            \
+    else if (nv == 2) ADMMQ_H3(Q, 2, false);       \
+    else ADMMQ_H3(Q, 1, false);                    \
   }
   switch (bits) {
-    case 1: ADMMQ_H3N(1, false); break;
-    case 2: ADMMQ_H3N(2, false); break;
-    case 3: ADMMQ_H3N(4, false); break;
-    case 4: ADMMQ_H3N(8, false); break;
-    default: ADMMQ_H3N(16, false); break;
+    case 1: ADMMQ_H3N(1); break;
+    case 2: ADMMQ_H3N(2); break;
+    case 3: ADMMQ_H3N(4); break;
+    case 4: ADMMQ_H3N(8); break;
+    default: ADMMQ_H3N(16); break;
   }
 #undef ADMMQ_H3N
 #undef ADMMQ_H3
@@ -1638,7 +1485,7 @@ void launch_mse_hist3(const ProbDesc* d, const QJob* q, const Chunk* chunks, int
 // separate finalize launch. (A one-block-per-CU margin would disable the fused form at
 // C3: 371 units against 2 x 256 resident blocks, 63 KB of LDS each.) The CU count is
 // looked up once per device.
-int hist3_fin_capacity(int ncand, int bits, int nv, bool pl) {
+int hist3_fin_capacity(int ncand, int bits, int nv) {
   constexpr int kMaxDev = 64;
   static std::once_flag once[kMaxDev];
   static int cus[kMaxDev];
@@ -1648,28 +1495,19 @@ int hist3_fin_capacity(int ncand, int bits, int nv, bool pl) {
     int n = 0;
     cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
   });
-  pl = pl && histl_ok(ncand, bits);
-  const size_t lds = pl ? histl_lds_bytes(ncand, bits) : hist3_lds_bytes(ncand, bits);
+  const size_t lds = hist3_lds_bytes(ncand, bits);
   int per = 0;
   hipError_t e = hipErrorInvalidValue;
-#define ADMMQ_OCC(Q, L)                                                                                             \
-  e = nv == 3   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 3, true, L>, kH3Threads, lds) \
-      : nv == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 2, true, L>, kH3Threads, lds) \
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 1, true, L>, kH3Threads, lds)
-  if (pl) {
-    switch (bits) {
-      case 2: ADMMQ_OCC(2, true); break;
-      case 3: ADMMQ_OCC(4, true); break;
-      default: ADMMQ_OCC(8, true); break;
-    }
-  } else {
-    switch (bits) {
-      case 1: ADMMQ_OCC(1, false); break;
-      case 2: ADMMQ_OCC(2, false); break;
-      case 3: ADMMQ_OCC(4, false); break;
-      case 4: ADMMQ_OCC(8, false); break;
-      default: ADMMQ_OCC(16, false); break;
-    }
+#define ADMMQ_OCC(Q) \
+  e = nv == 3   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 3, true>, kH3Threads, lds) \
+      : nv == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 2, true>, kH3Threads, lds) \
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mse_hist3<Q, 1, true>, kH3Threads, lds)
+  switch (bits) {
+    case 1: ADMMQ_OCC(1); break;
+    case 2: ADMMQ_OCC(2); break;
+    case 3: ADMMQ_OCC(4); break;
+    case 4: ADMMQ_OCC(8); break;
+    default: ADMMQ_OCC(16); break;
   }
 #undef ADMMQ_OCC
   return e == hipSuccess ? per * cus[dev] : 0;

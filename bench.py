@@ -421,8 +421,6 @@ def emulate_shards(a):
     _lib.check(lib.admmq_debug_set_ksplit_form(a.ksplit_form), "ksplit_form")
     _lib.check(lib.admmq_debug_set_ksplit_balance(*[int(v) for v in a.ksplit_bal.split(":")]), "ksplit_balance")
     _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
-    _lib.check(lib.admmq_debug_set_search_spread(a.search_spread), "search_spread")
-    _lib.check(lib.admmq_debug_set_search_pl(a.search_pl), "search_pl")
     if a.gemm_stage >= 0:
         _lib.check(lib.admmq_debug_set_gemm_stage(a.gemm_stage), "gemm_stage")
     N = a.emulate_world
@@ -555,12 +553,6 @@ def main():
     ap.add_argument("--fin-nv3", type=int, default=1, choices=[0, 1],
                     help="A/B: 1 (library default) = three float4 groups per search thread where that keeps the "
                          "finalize in the search launch (C4), 0 = at most two (separate finalize launch at C4)")
-    ap.add_argument("--search-spread", type=int, default=1, choices=[0, 1],
-                    help="A/B: 1 (library default) = a search launch of at most one block per CU takes 96 KB of LDS "
-                         "per block (spread over the CUs), 0 = its own LDS size")
-    ap.add_argument("--search-pl", type=int, default=1, choices=[0, 1, 2],
-                    help="A/B: stage-1 form of the search, 0 = merged thresholds, 1 (library default) = per level "
-                         "where a launch has at most one block per CU, 2 = per level always (same bits)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="multi-GPU readiness on ONE GPU: time every rank's LPT layer shard of an N-GPU run "
                          "(same code path, one after another) and report the busiest shard and the implied speed-up")
@@ -607,8 +599,6 @@ def main():
     if a.wide_min >= 0:
         _lib.check(lib.admmq_debug_set_wide_min_tiles(a.wide_min), "wide_min")
     _lib.check(lib.admmq_debug_set_fin_nv3(a.fin_nv3), "fin_nv3")
-    _lib.check(lib.admmq_debug_set_search_spread(a.search_spread), "search_spread")
-    _lib.check(lib.admmq_debug_set_search_pl(a.search_pl), "search_pl")
     if a.f32_kernel >= 0:
         _lib.check(lib.admmq_debug_set_f32_persistent(a.f32_kernel, a.f32_tiles), "f32_kernel")
     split = a.solve == "split"

@@ -291,7 +291,7 @@ int32_t admmq_epc_mu(const double* c, const double* s, int64_t n, double normY2,
                      void* stream);
 
 /* The R x R solves of the CP-ALS / EPC initialiser on one workgroup (the fp64 matrix in LDS,
- * 1 <= n <= 140), replacing tensorly parafac's torch.linalg.solve and cp_anc's eigendecomposition
+ * 1 <= n <= 136), replacing tensorly parafac's torch.linalg.solve and cp_anc's eigendecomposition
  * (source/parafac_epc.py:42, :61-74). Row-major device doubles; no host synchronisation.
  *   admmq_spd_solve64  X = F G^-1 (F, X: m x n; G: n x n SPD); *info (device int, may be NULL)
  *                      = 0, or 1 when G is not positive definite (X untouched).

@@ -169,38 +169,6 @@ def test_c4_fused_three_groups_equals_separate(torch_dev):
         assert np.array_equal(_bits(he), _bits(hb)) and np.array_equal(_bits(ue), _bits(ub)), pr[0]
 
 
-@pytest.mark.parametrize("shapes", [[(512, 1141)], [(512, 1141), (256, 566), (128, 278), (64, 134)]],
-                         ids=["lone_layer4", "shard_mix"])
-def test_search_forms_equal(torch_dev, shapes):
-    """The per-level stage 1 (k_mse_hist3<.., PL>: per-candidate bins, one suffix scan in the
-    last block) and the merged-threshold form give the same integers, hence the same H, U and
-    iteration counts bit for bit over 4 iterations: fused finalize and separate launch, spread
-    (one block per CU) and default placement. The launches hold at most one block per CU
-    (a lone layer4 factor, a small multi-GPU shard), where the library picks the per-level form."""
-    torch, dev = torch_dev
-    from admmq import admm_iteration_batched, _lib
-    g = torch.Generator().manual_seed(5)
-    base = []
-    for I, R in shapes:
-        B = torch.randn(R, 2 * R, generator=g) / (2 * R) ** 0.5
-        base.append((torch.randn(I, R, generator=g) * 0.1, torch.randn(I, R, generator=g),
-                     B @ B.T + 0.5 * torch.eye(R)))
-
-    def run(pl, spread, fused):
-        ps = [(H.to(dev), torch.zeros(H.shape, device=dev), F.to(dev), G.to(dev)) for (H, F, G) in base]
-        with _lib.search_form(pl, spread), _lib.fused_finalize(fused):
-            Hs, info = admm_iteration_batched(ps, 5, 0.0, 4, MSE, return_info=True)
-        return [(H.cpu().numpy(), p[1].cpu().numpy()) for H, p in zip(Hs, ps)], info.cpu().numpy()
-
-    ref, iref = run(0, 0, True)
-    assert (iref[:, 3] == 0).all() and (iref[:, 4] == 0).all()
-    for pl, spread, fused in ((2, 1, True), (2, 0, True), (2, 1, False), (1, 1, True), (0, 1, True)):
-        got, info = run(pl, spread, fused)
-        assert np.array_equal(info[:, :3], iref[:, :3]) and (info[:, 3] == 0).all(), (pl, spread, fused)
-        for (h, u), (hr, ur), sh in zip(got, ref, shapes):
-            assert np.array_equal(_bits(h), _bits(hr)) and np.array_equal(_bits(u), _bits(ur)), (pl, spread, fused, sh)
-
-
 def _llama_problem(torch, dev, I, J, R, seed):
     """2-way mode 0 of W (I, J): F = W B, G = B^T B (scripts/factorize.py:276-277)."""
     g = torch.Generator().manual_seed(seed)

@@ -117,7 +117,7 @@ def test_epc_mu_device_matches_oracle(R, seed):
         assert abs(got - ref) <= 1e-12 * max(abs(ref), 1e-300) or (ref == 0.0 and got == 0.0), (delta2, got, ref)
 
 
-@pytest.mark.parametrize("n,m", [(1, 3), (5, 9), (64, 1), (134, 64), (134, 9), (140, 130)])
+@pytest.mark.parametrize("n,m", [(1, 3), (5, 9), (64, 1), (134, 64), (134, 9), (136, 130)])
 def test_spd_solve64_vs_library(n, m):
     """The one-workgroup fp64 solve (csrc/epc_kernels.hip: Cholesky with the matrix in LDS,
     16-lane substitution groups) that replaces tensorly parafac's torch.linalg.solve
@@ -133,7 +133,7 @@ def test_spd_solve64_vs_library(n, m):
     assert _rel(X, ref) < 1e-11, _rel(X, ref)
 
 
-@pytest.mark.parametrize("n,m,seed", [(134, 64, 1), (134, 9, 2), (7, 5, 3), (140, 64, 4)])
+@pytest.mark.parametrize("n,m,seed", [(134, 64, 1), (134, 9, 2), (7, 5, 3), (136, 64, 4)])
 def test_epc_step64_vs_eigen_form(n, m, seed):
     """The EPC mode update on the device (Newton on Cholesky factors of G + mu I, no
     eigendecomposition) against the eigen form the oracle uses (oracle/epc_oracle.py:

@@ -43,12 +43,17 @@ pe.gram_mttkrp_f64, torch.linalg.eigh, torch.linalg.solve, pe.cp_anc = gm, eigh,
 pe.parafac_epc(W, R, als_maxiter=2, epc_maxiter=2, epc_rounds=1)   # warm-up (kernels, library handles)
 for k in calls:
     calls[k] = 0
+import ctypes  # noqa: E402
+from admmq import _lib as _l  # noqa: E402
+_ev = ctypes.c_ulonglong(0)
+_l.load().admmq_debug_epc_evals(ctypes.byref(_ev), 1)
 torch.cuda.synchronize()
 t0 = time.time()
 lam, Us = pe.parafac_epc(W, R, als_maxiter=50, epc_maxiter=50)
 torch.cuda.synchronize()
 t = time.time() - t0
-print(f"parafac_epc layer1.0.conv1 R={R}: {t:.2f} s; calls {calls}")
+_l.load().admmq_debug_epc_evals(ctypes.byref(_ev), 1)
+print(f"parafac_epc layer1.0.conv1 R={R}: {t:.2f} s; calls {calls}; EPC Cholesky evaluations {_ev.value}")
 G = torch.randn(R, 2 * R, device="cuda", dtype=torch.float64)
 G = G @ G.T
 F = torch.randn(64, R, device="cuda", dtype=torch.float64)
@@ -66,3 +71,40 @@ t0 = time.time()
 w, fs = pe.parafac(W, R, tol=1e-5, n_iter_max=50, normalize_factors=True)
 torch.cuda.synchronize()
 print(f"  parafac alone (50 its): {time.time() - t0:.2f} s")
+
+# the EPC step alone: Cholesky evaluations per call and device time per call, on the G / F of
+# one mode of the factors just computed (warm start = the previous call's mu)
+import ctypes  # noqa: E402
+from admmq import _lib, panel  # noqa: E402
+from admmq.als import gram_mttkrp_f64  # noqa: E402
+lib = _lib.load()
+Y = W.permute(*sorted(range(3), key=lambda m: W.shape[m])).contiguous()
+fs = [u.contiguous() for u in Us]
+fs = [fs[m] for m in sorted(range(3), key=lambda m: W.shape[m])]
+F, G = orig_gm(Y, fs, 1)
+normY2 = float(torch.sum(Y * Y))
+s = torch.linalg.eigvalsh(G)
+for label, d2 in (("mu ~ 0 (flat)", None), ("mu ~ s", 1.0)):
+    X0 = panel.spd_solve64(G, F)
+    e0 = normY2 - float(torch.sum(F * X0))
+    delta2 = e0 * 1.0001 if d2 is None else e0 + 0.5 * (normY2 - e0)
+    mu = torch.zeros((), dtype=torch.float64, device="cuda")
+    cnt = ctypes.c_ulonglong(0)
+    lib.admmq_debug_epc_evals(ctypes.byref(cnt), 1)
+    panel.epc_step64(G, F, normY2, delta2, mu)   # cold
+    torch.cuda.synchronize()
+    lib.admmq_debug_epc_evals(ctypes.byref(cnt), 1)
+    cold = cnt.value
+    t0 = time.time()
+    for _ in range(20):
+        panel.epc_step64(G, F, normY2, delta2, mu)   # warm (at the root)
+    torch.cuda.synchronize()
+    dt = (time.time() - t0) / 20
+    lib.admmq_debug_epc_evals(ctypes.byref(cnt), 1)
+    print(f"  epc_step64 {label}: mu {float(mu):.3e} (s {float(s.min()):.3e} .. {float(s.max()):.3e}); "
+          f"evals cold {cold}, warm {cnt.value / 20:.1f}; {dt * 1e3:.3f} ms per warm call")
+t0 = time.time()
+for _ in range(50):
+    panel.spd_solve64(G, F)
+torch.cuda.synchronize()
+print(f"  spd_solve64: {(time.time() - t0) / 50 * 1e3:.3f} ms per call")

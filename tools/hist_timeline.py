@@ -19,8 +19,6 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--shapes", default="", help="I:R,I:R,... instead of the resnet18 factors of --mode")
-ap.add_argument("--spread", type=int, default=-1, help="admmq_debug_set_search_spread (default: library's)")
-ap.add_argument("--pl", type=int, default=-1, help="admmq_debug_set_search_pl (default: library's)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 g = torch.Generator().manual_seed(0)
@@ -34,10 +32,6 @@ for I, R in shapes:
     H = torch.randn(I, R, generator=g).to(dev) * 0.1
     U = torch.zeros(I, R, device=dev)
     probs.append((H, U, F, G))
-if a.spread >= 0:
-    _lib.load().admmq_debug_set_search_spread(a.spread)
-if a.pl >= 0:
-    _lib.load().admmq_debug_set_search_pl(a.pl)
 admm_iteration_batched(probs, a.iters, 0.0, 4, "tensor_mseminmax_symmetric", check_spd=False)
 torch.cuda.synchronize()
 lib = _lib.load()

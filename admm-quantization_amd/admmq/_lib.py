@@ -116,7 +116,8 @@ def load() -> ctypes.CDLL:
         "admmq_spd_solve64": (I32, [P, P, I64, I64, P, P, P]),
         "admmq_debug_epc_evals": (I32, [P, I32]),
         "admmq_debug_spd_trace": (I32, [P]),
-        "admmq_epc_step64": (I32, [P, P, I64, I64, ctypes.c_double, ctypes.c_double, P, P, P, P]),
+        "admmq_debug_epc_trace": (I32, [P]),
+        "admmq_epc_step64": (I32, [P, P, I64, I64, ctypes.c_double, ctypes.c_double, P, P, P, P, P]),
         "admmq_debug_hist_cu": (I32, [P, I32]),
         "admmq_debug_set_fin_capacity": (I32, [I32]),
         "admmq_debug_set_fin_nv3": (I32, [I32]),

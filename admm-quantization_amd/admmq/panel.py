@@ -156,8 +156,8 @@ def spd_solve64(G: torch.Tensor, F: torch.Tensor) -> torch.Tensor:
 
 def epc_step64(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor) -> torch.Tensor:
     """One EPC mode update of musco ``cp_anc`` on the device: ``F (G + mu I)^-1`` with ``mu >= 0``
-    the root of the error equation (``csrc/epc_kernels.hip``: Newton steps on Cholesky factors
-    of ``G + mu I``, no eigendecomposition). ``mu`` is a 0-dim float64 device tensor: the warm
+    the root of the error equation (``csrc/epc_kernels.hip``: G tridiagonalised once, then
+    safeguarded Newton steps on tridiagonal LDL^T recurrences, no eigendecomposition). ``mu`` is a 0-dim float64 device tensor: the warm
     start in, the root out (updated in place). n <= SPD_SMALL_MAX; no host synchronisation."""
     n = G.shape[0]
     if G.dtype != torch.float64 or F.dtype != torch.float64 or G.shape != (n, n) or F.dim() != 2 or F.shape[1] != n:
@@ -168,7 +168,9 @@ def epc_step64(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, m
         raise ValueError("admmq.panel.epc_step64: mu must be a float64 scalar tensor on F's device")
     G, F = G.contiguous(), F.contiguous()
     X = torch.empty(F.shape, dtype=torch.float64, device=F.device)
+    work = torch.empty(F.shape, dtype=torch.float64, device=F.device)
     _lib.check(_lib.load().admmq_epc_step64(_lib.ptr(G), _lib.ptr(F), F.shape[0], n, float(normY2), float(delta2),
-                                            _lib.ptr(mu), _lib.ptr(X), None, _lib.stream_handle(F.device)),
+                                            _lib.ptr(mu), _lib.ptr(X), _lib.ptr(work), None,
+                                            _lib.stream_handle(F.device)),
                "epc_step64")
     return X

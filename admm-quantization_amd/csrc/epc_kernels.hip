@@ -333,53 +333,410 @@ __global__ __launch_bounds__(kSpdThreads) void k_spd_solve64(const double* __res
   if (threadIdx.x == 0 && info) *info = 0;
 }
 
-// Diagnostics (admmq_debug_epc_evals): evaluations (inverses) made by k_epc_step64 since the
-// last reset
+// Diagnostics (admmq_debug_epc_evals): evaluations of e(mu) made by k_epc_step64 since the
+// last reset; TRACE builds (admmq_debug_epc_trace): s_memrealtime of the last k_epc_step64 at
+// {start, G in LDS, tridiagonal, Z = F Q, search done, X written}
 __device__ unsigned long long g_epc_evals = 0ull;
+__device__ unsigned long long g_epc_trace[16];   // [8 + k]: tridiagonalisation phase sums (wave 0's view)
+#define ADMMQ_EPC_STAMP(k) \
+  if (ADMMQ_TRACE && threadIdx.x == 0) g_epc_trace[k] = ADMMQ_NOW();
 
-// e(mu), e'(mu) and X = F (G + mu I)^-1 (into X when `store`); false if G + mu I is not SPD.
-// With A = G + mu I: <F, X> and ||X||^2 give e = normY2 - <F, X> - mu ||X||^2 (the eigen form
-// normY2 - sum_j c_j (s_j + 2 mu) / (s_j + mu)^2), and e' = 2 mu <X, X A^-1>.
-constexpr int kEpcThreads = 1024;   // (512 threads: no spills, but the rank-8 updates at half the width: 6.3 vs 5.4 s per parafac_epc)
-__device__ __forceinline__ bool epc_eval(const double* __restrict__ G, const double* __restrict__ F, int m, int n,
-                                         double mu, double normY2, double* A, double* sP, double* Cb, double* red,
-                                         double* X, double& e, double& de) {
-  if (threadIdx.x == 0) atomicAdd(&g_epc_evals, 1ull);
-  if (!spd_inverse_lds<kEpcThreads>(G, n, mu, A, sP, Cb)) return false;
-  double fx = 0.0, xx = 0.0, ww = 0.0;
-  const int c = threadIdx.x & (kSpdCols - 1);
-  for (int r0 = 0; r0 < m; r0 += kEpcThreads / kSpdCols) {   // X = F A^-1 (stored), <F, X>, ||X||^2
-    const int row = r0 + (int)(threadIdx.x / kSpdCols);
-    if (r0 + 4 * (int)(threadIdx.x >> 6) >= m) continue;   // every row of this wave past the end
-    double f[kSpdPer], x[kSpdPer];
-    spd_load_row(F, row, m, n, f);
-    spd_row_times(A, n, f, x);
+// ---------------------------------------------------------------------------
+// The EPC mode update through one tridiagonal reduction per call. G = Q T Q^T (Householder,
+// T symmetric tridiagonal, Q = H_0 ... H_{n-3}) once; with Z = F Q every evaluation of the
+// error equation is a set of independent tridiagonal recurrences:
+//   <F, X> = z (T + mu)^-1 z^T,  ||X||^2 = z (T + mu)^-2 z^T,  <X, X (G + mu)^-1> = z (T + mu)^-3 z^T
+// summed over the rows z of Z. With T + mu = L D L^T (L unit lower bidiagonal) and u = L^-1 z,
+// s(mu) = sum_i u_i^2 / D_i is the first; the other two are -s' and s'' / 2, carried through
+// the same forward recurrence as derivatives in mu (D', D'', L', L'' once per evaluation, by
+// one thread; u', u'' per row). One evaluation is O(m n) work with an n-step dependency
+// chain (a few microseconds), where an explicit (G + mu I)^-1 was O(n^3) on one workgroup;
+// the final X = (Z (T + mu)^-1) Q^T is one forward / backward pass and the reflectors applied
+// in reverse.
+constexpr int kEpcThreads = 1024;   // (512: 256 VGPRs, but half the lanes on the rank-2 updates and two passes over
+                                    // 64 rows in the reflector products: 0.79 vs 0.71 ms per step)
+                                   // 128 VGPRs the compiler serialised them through one register pair)
+
+// Householder tridiagonalisation of the symmetric A (LDS, n x n, lda = n + 1) in place:
+// dd (diagonal), ee (off-diagonal), tau_k and v_k (v_k[k + 1] = 1, stored in row k from
+// column k + 1: that row is not touched after step k). Step k: p = tau A22 v,
+// w = p - (tau / 2)(p . v) v, A22 -= v w^T + w v^T on the trailing (n - k - 1)^2 block (both
+// triangles). Two workgroup barriers per step: the reflector of step k + 1 is formed by wave 0
+// right after its own rows of step k's update (it owns row k + 1), into the other half of the
+// double-buffered vb.
+// Cross-lane sums without LDS round trips: DPP within a row of 16 lanes (xor 1, xor 2, half
+// mirror, mirror: every lane of the row ends with the row's sum), v_readlane across the four
+// rows. At this size every step is a latency chain; a ds_bpermute shuffle costs an LDS round
+// trip per level.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double sum16(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return v;
+}
+__device__ __forceinline__ double sum64(double v) {   // the wave's sum, in every lane
+  v = sum16(v);
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+__device__ __forceinline__ void tri_reflector(double* A, int n, int k, double* vb, double* tau, double* dd,
+                                              double* ee) {
+  const int lane = threadIdx.x & 63, lda = spd_lda(n);
+  double* row = A + k * lda;
+  const double alpha = row[k + 1], dk = row[k];
+  double x[3], sig = 0.0;
 #pragma unroll
-    for (int q = 0; q < kSpdPer; ++q) { fx += f[q] * x[q]; xx += x[q] * x[q]; }
-    if (row < m)
-#pragma unroll
-      for (int q = 0; q < kSpdPer; ++q) {
-        const int i = c + kSpdCols * q;
-        if (i < n) X[(size_t)row * n + i] = x[q];
-      }
+  for (int h = 0; h < 3; ++h) {
+    const int j = k + 2 + lane + 64 * h;
+    const double xr = row[min(j, n - 1)];
+    x[h] = j < n ? xr : 0.0;
+    sig += x[h] * x[h];
   }
-  if (mu > 0.0) {   // <X, X A^-1>, X read back (this thread's own stores)
-    for (int r0 = 0; r0 < m; r0 += kEpcThreads / kSpdCols) {
-      const int row = r0 + (int)(threadIdx.x / kSpdCols);
-      if (r0 + 4 * (int)(threadIdx.x >> 6) >= m) continue;
-      double x[kSpdPer], y[kSpdPer];
-      spd_load_row(X, row, m, n, x);
-      spd_row_times(A, n, x, y);
+  sig = sum64(sig);
+  double t = 0.0, beta = alpha, scale = 0.0;
+  if (sig > 0.0) {
+    const double nrm = sqrt(alpha * alpha + sig);
+    beta = alpha <= 0.0 ? nrm : -nrm;
+    t = (beta - alpha) / beta;
+    scale = 1.0 / (alpha - beta);
+  }
 #pragma unroll
-      for (int q = 0; q < kSpdPer; ++q) ww += x[q] * y[q];
+  for (int h = 0; h < 3; ++h) {
+    const int j = k + 2 + lane + 64 * h;
+    if (j < n) {
+      const double v = x[h] * scale;
+      vb[j - k - 1] = v;
+      row[j] = v;
     }
   }
-  fx = spd_block_sum<kEpcThreads>(fx, red);
-  xx = spd_block_sum<kEpcThreads>(xx, red);
-  ww = spd_block_sum<kEpcThreads>(ww, red);
-  e = normY2 - fx - mu * xx;
-  de = 2.0 * mu * ww;
-  return true;
+  if (lane == 0) {
+    dd[k] = dk;
+    vb[0] = 1.0;
+    row[k + 1] = 1.0;
+    tau[k] = t;
+    ee[k] = beta;
+  }
+}
+
+constexpr int kTriBatch = 3;   // update rows loaded before their stores
+
+template <int NT>
+__device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double* ee, double* tau, double* vb2,
+                                            double* pb) {
+  constexpr int kWaves = NT / 64, kGroups = NT / 16;
+  constexpr int kRowsPerWave = (kSpdSmallMax + kWaves - 1) / kWaves;      // update rows per wave
+  constexpr int kRowsPerGroup = (kSpdSmallMax + kGroups - 1) / kGroups;   // matvec rows per 16-lane group
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lda = spd_lda(n);
+  const int g = tid >> 4, c = tid & 15;
+  if (n >= 3 && w == 0) tri_reflector(A, n, 0, vb2, tau, dd, ee);
+  unsigned long long ph[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tp = ADMMQ_NOW();
+#define ADMMQ_TRI_PH(k)                               \
+  if (ADMMQ_TRACE) {                                  \
+    const unsigned long long tn_ = ADMMQ_NOW();       \
+    ph[k] += tn_ - tp;                                \
+    tp = tn_;                                         \
+  }
+  for (int k = 0; k + 3 <= n; ++k) {
+    const int m = n - k - 1;
+    const double* vb = vb2 + (k & 1) * kSpdSmallMax;
+    __syncthreads();   // v_k, tau_k (and step k - 1's update) visible
+    ADMMQ_TRI_PH(0);
+    const double t = tau[k];
+    {   // p = tau A22 v: the group's rows' partial sums first, then their 16-lane sums together
+      double vq[kSpdPer];
+#pragma unroll
+      for (int q = 0; q < kSpdPer; ++q) {
+        const int j = c + 16 * q;
+        const double x = vb[min(j, m - 1)];
+        vq[q] = j < m ? x : 0.0;
+      }
+      double acc[kRowsPerGroup];
+#pragma unroll
+      for (int b = 0; b < kRowsPerGroup; ++b) {
+        const int r = k + 1 + g + kGroups * b;
+        const double* Ar = A + min(r, n - 1) * lda + k + 1;
+        double a0 = Ar[min(c, m - 1)] * vq[0], a1 = Ar[min(c + 16, m - 1)] * vq[1], a2 = Ar[min(c + 32, m - 1)] * vq[2];
+#pragma unroll
+        for (int q = 3; q < kSpdPer; q += 3) {
+          a0 = fma(Ar[min(c + 16 * q, m - 1)], vq[q], a0);
+          if (q + 1 < kSpdPer) a1 = fma(Ar[min(c + 16 * (q + 1), m - 1)], vq[q + 1], a1);
+          if (q + 2 < kSpdPer) a2 = fma(Ar[min(c + 16 * (q + 2), m - 1)], vq[q + 2], a2);
+        }
+        acc[b] = (a0 + a1) + a2;
+      }
+#pragma unroll
+      for (int b = 0; b < kRowsPerGroup; ++b) acc[b] = sum16(acc[b]);
+#pragma unroll
+      for (int b = 0; b < kRowsPerGroup; ++b) {
+        const int r = k + 1 + g + kGroups * b;
+        if (c == 0 && r < n) pb[r - k - 1] = t * acc[b];
+      }
+    }
+    ADMMQ_TRI_PH(1);
+    __syncthreads();
+    ADMMQ_TRI_PH(2);
+    double vj[3], wj[3], pv = 0.0;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int i = lane + 64 * h;
+      const double xv = vb[min(i, m - 1)], xw = pb[min(i, m - 1)];
+      vj[h] = i < m ? xv : 0.0;
+      wj[h] = i < m ? xw : 0.0;
+      pv += vj[h] * wj[h];
+    }
+    const double K = 0.5 * t * sum64(pv);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) wj[h] -= K * vj[h];
+    // A22 -= v w^T + w v^T: rows r = k + 1 + w + kWaves b of this wave, lanes on columns; a batch
+    // of rows' loads before its stores (the compiler cannot tell the rows apart)
+#pragma unroll
+    for (int b0 = 0; b0 < kRowsPerWave; b0 += kTriBatch) {
+      double a[kTriBatch][3];
+#pragma unroll
+      for (int b = 0; b < kTriBatch; ++b) {
+        const double* Ar = A + min(k + 1 + w + kWaves * (b0 + b), n - 1) * lda + k + 1;
+#pragma unroll
+        for (int h = 0; h < 3; ++h) a[b][h] = Ar[min(lane + 64 * h, m - 1)];
+      }
+#pragma unroll
+      for (int b = 0; b < kTriBatch; ++b) {
+        const int r = k + 1 + w + kWaves * (b0 + b);
+        if (b0 + b < kRowsPerWave && r < n) {
+          const double vi = vb[r - k - 1], wi = pb[r - k - 1] - K * vi;
+          double* Ar = A + r * lda + k + 1;
+#pragma unroll
+          for (int h = 0; h < 3; ++h) {
+            const int i = lane + 64 * h;
+            if (i < m) Ar[i] = fma(-vi, wj[h], fma(-wi, vj[h], a[b][h]));
+          }
+        }
+      }
+    }
+    ADMMQ_TRI_PH(3);
+    if (w == 0 && k + 4 <= n) {   // wave 0 updated row k + 1 (its first row): the next reflector
+      asm volatile("" ::: "memory");
+      tri_reflector(A, n, k + 1, vb2 + ((k + 1) & 1) * kSpdSmallMax, tau, dd, ee);
+    }
+    ADMMQ_TRI_PH(4);
+  }
+#undef ADMMQ_TRI_PH
+  if (ADMMQ_TRACE && tid == 0)
+    for (int q = 0; q < 5; ++q) g_epc_trace[8 + q] = ph[q];
+  __syncthreads();
+  if (tid == 0) {
+    if (n >= 2) {
+      dd[n - 2] = A[(n - 2) * lda + n - 2];
+      ee[n - 2] = A[(n - 2) * lda + n - 1];
+    }
+    dd[n - 1] = A[(n - 1) * lda + n - 1];
+  }
+  __syncthreads();
+}
+
+// One row of F -> F Q (dir = +1: H_0 first) or one row of Y -> Y Q^T (dir = -1: H_{n-3}
+// first), 16 lanes per row, lane c holding coordinates c + 16 q
+__device__ __forceinline__ void tri_apply_q(const double* A, int n, const double* tau, int dir, double (&f)[kSpdPer]) {
+  const int c = threadIdx.x & 15, lda = spd_lda(n);
+  for (int s = 0; s + 3 <= n; ++s) {
+    const int k = dir > 0 ? s : n - 3 - s;
+    const double* v = A + k * lda;   // v_k at columns k + 1 ..
+    double vq[kSpdPer];
+#pragma unroll
+    for (int q = 0; q < kSpdPer; ++q) {
+      const int j = c + 16 * q;
+      const double x = v[min(max(j, k + 1), n - 1)];   // (loaded unconditionally, then selected)
+      vq[q] = (j > k && j < n) ? x : 0.0;
+    }
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kSpdPer; q += 3) {
+      d0 = fma(f[q], vq[q], d0);
+      if (q + 1 < kSpdPer) d1 = fma(f[q + 1], vq[q + 1], d1);
+      if (q + 2 < kSpdPer) d2 = fma(f[q + 2], vq[q + 2], d2);
+    }
+    const double d = sum16((d0 + d1) + d2) * tau[k];
+#pragma unroll
+    for (int q = 0; q < kSpdPer; ++q) f[q] = fma(-d, vq[q], f[q]);
+  }
+}
+
+// The LDL^T recurrence of T + mu I with its first and second derivatives in mu (thread 0),
+// packed per step i (8 doubles, two 16-byte loads and one more): P[i] = {L_{i-1}, L_{i-1}',
+// L_{i-1}'' (0 for i = 0), 1 / D_i, D_i' / D_i^2, D_i'' / D_i^2 - 2 D_i'^2 / D_i^3}. The
+// dependency chain per step is one division and one fma (D_{i+1} = d_{i+1} + mu - e_i^2 / D_i,
+// fp64 ops cost ~30 clocks each in a chain); d and e come one step ahead, everything else is
+// off the chain. false if a pivot is not positive and finite.
+constexpr int kTriP = 8;
+constexpr int kTriChunk = 4;                                                     // recurrence steps per prefetched chunk
+constexpr int kTriPad = (kSpdSmallMax + 2 * kTriChunk - 1) / (2 * kTriChunk) * (2 * kTriChunk);   // P rows (144)
+__device__ __forceinline__ bool tri_ldl(const double* __restrict__ dd, const double* __restrict__ ee, int n, double mu,
+                                        double* __restrict__ P) {
+  double D = dd[0] + mu, D1 = 1.0, D2 = 0.0, L = 0.0, L1 = 0.0, L2 = 0.0;
+  double e = ee[0], an = dd[min(1, n - 1)] + mu;
+  bool bad = false;   // (no branch per step: a bad pivot only spoils the rest, which is then unused)
+#pragma unroll 2
+  for (int i = 0; i < n; ++i) {
+    bad |= !(D > 0.0) || !(D < __builtin_huge_val());
+    const double e_next = ee[min(i + 1, kSpdSmallMax - 1)], a_next = dd[min(i + 2, n - 1)] + mu;   // (prefetch)
+    const double gi = 1.0 / D;
+    const double g2 = gi * gi;
+    double* Pi = P + kTriP * i;
+    Pi[0] = L;
+    Pi[1] = L1;
+    Pi[2] = L2;
+    Pi[3] = gi;
+    Pi[4] = D1 * g2;
+    Pi[5] = D2 * g2 - 2.0 * D1 * D1 * g2 * gi;
+    L = e * gi;
+    L1 = -e * D1 * g2;
+    L2 = e * (2.0 * D1 * D1 * g2 * gi - D2 * g2);
+    D = fma(-e * e, gi, an);   // the chain: one division and one fma per step
+    D1 = fma(-e, L1, 1.0);
+    D2 = -e * L2;
+    e = e_next;
+    an = a_next;
+  }
+  for (int i = n; i < kTriPad; ++i)   // zero steps past n: the row recurrences run whole chunks
+#pragma unroll
+    for (int q = 0; q < 6; ++q) P[kTriP * i + q] = 0.0;
+  return !bad;
+}
+
+// Block sums of three values (every thread's; the results in every thread)
+template <int NT>
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = a;
+    red[NT / 64 + (threadIdx.x >> 6)] = b;
+    red[2 * NT / 64 + (threadIdx.x >> 6)] = c;
+  }
+  __syncthreads();
+  a = b = c = 0.0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    a += red[w];
+    b += red[NT / 64 + w];
+    c += red[2 * NT / 64 + w];
+  }
+  __syncthreads();   // red reused
+}
+
+// s, s', s'' of one row z (Zt: n x m, column `row`) from the packed coefficients P at the
+// current mu. z is read a chunk of kTriChunk ahead and P one step ahead of the recurrence;
+// the empty asm between steps keeps the compiler from hoisting every step's P loads to the
+// top of the chunk (they would take ~100 VGPRs).
+struct TriCoef { double L, L1, L2, a1, a2, a3; };
+__device__ __forceinline__ TriCoef tri_coef(const double* P, int i) {
+  const double* Pi = P + kTriP * i;
+  return TriCoef{Pi[0], Pi[1], Pi[2], Pi[3], Pi[4], Pi[5]};
+}
+__device__ __forceinline__ void tri_row_sums(const double* __restrict__ Zt, int m, int n, int row, const double* P,
+                                             double& s0, double& s1, double& s2) {
+  // every recurrence is one fma deep per step (the terms from the other chains formed off
+  // it), and the sums alternate between two accumulators: a chained fp64 op costs ~30 clocks
+  double u = 0.0, u1 = 0.0, u2 = 0.0;
+  double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0}, a2[2] = {0.0, 0.0};
+  TriCoef cur = tri_coef(P, 0);
+  auto steps = [&](const double (&zz)[kTriChunk], int i0) {   // (steps past n: P = 0, so no terms)
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) {
+      const int i = i0 + q;
+      const TriCoef nxt = tri_coef(P, min(i + 1, kTriPad - 1));
+      const double c2 = fma(2.0 * cur.L1, u1, cur.L2 * u), c1 = cur.L1 * u;
+      u2 = fma(-cur.L, u2, -c2);
+      u1 = fma(-cur.L, u1, -c1);
+      u = fma(-cur.L, u, zz[q]);
+      const double uu = u * u, uu1 = u * u1;
+      const double t0 = uu * cur.a1;
+      const double t1 = fma(2.0 * uu1, cur.a1, -uu * cur.a2);
+      const double t2 = fma(2.0 * fma(u1, u1, u * u2), cur.a1, fma(-4.0 * uu1, cur.a2, -uu * cur.a3));
+      a0[q & 1] += t0;
+      a1[q & 1] += t1;
+      a2[q & 1] += t2;
+      cur = nxt;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // two chunk buffers in turn: one being read while the other's loads are in flight (the
+  // indices clamped, not predicated: straight-line loads keep counted vmcnt waits)
+  double za[kTriChunk], zb[kTriChunk];
+#pragma unroll
+  for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(q, n - 1) * m + row];
+  for (int i0 = 0; i0 < n; i0 += 2 * kTriChunk) {
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) zb[q] = Zt[(size_t)min(i0 + kTriChunk + q, n - 1) * m + row];
+    steps(za, i0);
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(i0 + 2 * kTriChunk + q, n - 1) * m + row];
+    steps(zb, i0 + kTriChunk);
+  }
+  s0 += a0[0] + a0[1];
+  s1 += a1[0] + a1[1];
+  s2 += a2[0] + a2[1];
+}
+
+// Y = Z (T + mu I)^-1 for one row: forward (u / D) from Zt into Wt, backward from Wt into Zt;
+// both transposed (n x m), chunks read ahead as in tri_row_sums
+__device__ __forceinline__ void tri_row_solve(double* __restrict__ Zt, double* __restrict__ Wt, int m, int n, int row,
+                                              const double* P) {
+  double u = 0.0;
+  auto fwd = [&](const double (&zz)[kTriChunk], int i0) {
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) {
+      const int i = i0 + q;
+      if (i < n) {
+        u = fma(-P[kTriP * i], u, zz[q]);   // (L_{-1} = 0)
+        Wt[(size_t)i * m + row] = u * P[kTriP * i + 3];
+      }
+    }
+  };
+  double za[kTriChunk], zb[kTriChunk];
+#pragma unroll
+  for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(q, n - 1) * m + row];
+  for (int i0 = 0; i0 < n; i0 += 2 * kTriChunk) {
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) zb[q] = Zt[(size_t)min(i0 + kTriChunk + q, n - 1) * m + row];
+    fwd(za, i0);
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(i0 + 2 * kTriChunk + q, n - 1) * m + row];
+    fwd(zb, i0 + kTriChunk);
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // this thread's Wt stores complete before it reads them back
+  double y = 0.0;
+  auto bwd = [&](const double (&ww)[kTriChunk], int i1) {
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) {
+      const int i = i1 - q;
+      if (i >= 0) {
+        y = i + 1 < n ? fma(-P[kTriP * (i + 1)], y, ww[q]) : ww[q];
+        Zt[(size_t)i * m + row] = y;
+      }
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kTriChunk; ++q) za[q] = Wt[(size_t)max(n - 1 - q, 0) * m + row];
+  for (int i1 = n - 1; i1 >= 0; i1 -= 2 * kTriChunk) {
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) zb[q] = Wt[(size_t)max(i1 - kTriChunk - q, 0) * m + row];
+    bwd(za, i1);
+#pragma unroll
+    for (int q = 0; q < kTriChunk; ++q) za[q] = Wt[(size_t)max(i1 - 2 * kTriChunk - q, 0) * m + row];
+    bwd(zb, i1 - kTriChunk);
+  }
 }
 
 // mu to 1e-12 relative: X = F (G + mu I)^-1 moves by at most mu_err / (lambda_min + mu) <= 1e-12
@@ -389,35 +746,63 @@ constexpr double kEpcMuTol = 1e-12;
 __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __restrict__ G, const double* __restrict__ F,
                                                             int m, int n, double normY2, double delta2,
                                                             double* __restrict__ mu_io, double* __restrict__ X,
-                                                            int* __restrict__ info) {
+                                                            double* __restrict__ Zt, int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) double A[];
-  __shared__ double sP[kGJ * kGJ];
-  __shared__ double Cb[kSpdSmallMax * kGJ];
-  __shared__ double red[kSpdThreads / 64];   // (>= the epc kernel's waves)
+  __shared__ double dd[kSpdSmallMax], ee[kSpdSmallMax], tau[kSpdSmallMax];
+  __shared__ __attribute__((aligned(16))) double cf[kTriP * kTriPad];   // the tridiagonalisation's vb (2 x n) and pb, then the LDL coefficients
+  __shared__ double red[3 * kEpcThreads / 64];
+  __shared__ int s_ok;
+  const int tid = threadIdx.x, lda = spd_lda(n);
+  ADMMQ_EPC_STAMP(0);
   double tr = 0.0;   // trace(G) / n: the scale of the bracket's first step
-  for (int i = threadIdx.x; i < n; i += kEpcThreads) tr += G[(size_t)i * n + i];
-  tr = spd_block_sum<kEpcThreads>(tr, red) / (double)n;
+  for (int e = tid; e < n * n; e += kEpcThreads) {
+    const int i = e / n, k = e - i * n;
+    const double v = G[e];
+    A[i * lda + k] = v;
+    if (i == k) tr += v;
+  }
+  {
+    double z1 = 0.0, z2 = 0.0;
+    block_sum3<kEpcThreads>(tr, z1, z2, red);   // (its first barrier also publishes A)
+  }
+  tr /= (double)n;
+  ADMMQ_EPC_STAMP(1);
+  tridiag_lds<kEpcThreads>(A, n, dd, ee, tau, cf, cf + 2 * kSpdSmallMax);
+  ADMMQ_EPC_STAMP(2);
+  // Z = F Q, stored transposed (Zt[i * m + row]: the row recurrences read it coalesced)
+  for (int r0 = 0; r0 < m; r0 += kEpcThreads / 16) {
+    const int row = r0 + (tid >> 4), c = tid & 15;
+    if (r0 + 4 * (tid >> 6) >= m) continue;   // every row of this wave past the end
+    double f[kSpdPer];
+    spd_load_row(F, row, m, n, f);
+    tri_apply_q(A, n, tau, +1, f);
+    if (row < m)
+#pragma unroll
+      for (int q = 0; q < kSpdPer; ++q) {
+        const int j = c + 16 * q;
+        if (j < n) Zt[(size_t)j * m + row] = f[q];
+      }
+  }
+  ADMMQ_EPC_STAMP(3);
   const double warm = *mu_io;
-  // One evaluation site (a state machine: every branch below is uniform over the workgroup):
+  // The search (a state machine in LDS, thread 0 deciding between evaluations; every branch
+  // below uniform over the workgroup):
   //   WARM   the warm start, when > 0: e < delta2 puts the root above it (mu > 0 for sure);
   //   ZERO   mu = 0: e(0) >= delta2 means the LS step keeps the error (mu = 0, done);
   //   GROW   no upper end yet: from max(lo, trace / n 2^-20), doubling / Newton steps;
-  //   NEWTON safeguarded Newton inside [lo, hi] until the step is below fp64 resolution, the
-  //          bracket has collapsed or e is at its rounding floor (e is flat near mu = 0,
-  //          e'(0) = 0, so a small |e - delta2| alone does not fix mu: the step decides);
-  //   FINAL  one more evaluation when X is not that of the returned mu.
-  enum { WARM, ZERO, GROW, NEWTON, FINAL, DONE };
-  // the search state lives in LDS (uniform; thread 0 updates it between evaluations), so the
-  // evaluation's registers are not shared with it (128 VGPRs at 1024 threads)
-  struct St { double e, de, mu, lo, hi, xmu, at; int state, have, need0; };
+  //   NEWTON safeguarded Newton inside [lo, hi] until the step is below kEpcMuTol, the bracket
+  //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
+  //          a small |e - delta2| alone does not fix mu: the step decides).
+  enum { WARM, ZERO, GROW, NEWTON, DONE };
+  struct St { double e, de, mu, lo, hi, at; int state, have, need0; };
   __shared__ St st;
-  if (threadIdx.x == 0) {
-    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val(); st.xmu = -1.0;
+  if (tid == 0) {
+    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val();
     st.state = warm > 0.0 ? WARM : ZERO; st.have = 0; st.need0 = 1;
   }
-  __syncthreads();
+  unsigned long long ev_ph[3] = {0ull, 0ull, 0ull};   // (TRACE: thread 0's LDL, row sums, block sum)
   for (int guard = 0; guard < 400; ++guard) {
-    if (threadIdx.x == 0) {   // where to evaluate next (or DONE)
+    if (tid == 0) {   // where to evaluate next (or DONE)
       for (;;) {
         const int state = st.state;
         if (state == WARM) { st.at = warm; break; }
@@ -427,35 +812,44 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
           if (st.have && st.de > 0.0) {   // a Newton step from below (lands above the root: e convex near it)
             const double nx = st.mu - (st.e - delta2) / st.de;
             if (nx > st.mu && nx < at) at = nx;
-            if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = FINAL; continue; }   // converged from below
+            if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = DONE; break; }   // converged from below
           }
-          if (!(at < 1e300)) { st.state = FINAL; continue; }
+          if (!(at < 1e300)) { st.state = DONE; break; }
           st.at = at;
           break;
         }
         if (state == NEWTON) {
-          if (!(st.hi - st.lo > kEpcMuTol * st.hi)) { st.state = FINAL; continue; }   // collapsed bracket
+          if (!(st.hi - st.lo > kEpcMuTol * st.hi)) { st.state = DONE; break; }   // collapsed bracket
           double nx = st.de > 0.0 ? st.mu - (st.e - delta2) / st.de : -1.0;
           if (!(nx > st.lo && nx < st.hi)) nx = 0.5 * (st.lo + st.hi);
-          if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = FINAL; continue; }   // converged
+          if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = DONE; break; }   // converged
           st.at = nx;
-          break;
-        }
-        if (state == FINAL) {
-          if (!st.have || st.xmu == st.mu) { st.state = DONE; break; }
-          st.at = st.mu;
           break;
         }
         break;   // DONE
       }
+      if (st.state != DONE) atomicAdd(&g_epc_evals, 1ull);
     }
-    __syncthreads();
+    if (tid == 0 && st.state != DONE) {   // the recurrence's coefficients there
+      const unsigned long long t0 = ADMMQ_NOW();
+      s_ok = tri_ldl(dd, ee, n, st.at, cf) ? 1 : 0;
+      ev_ph[0] += ADMMQ_NOW() - t0;
+    }
+    __syncthreads();   // (also: Zt written, before the first evaluation)
     if (st.state == DONE) break;
-    double en, dn;
     const double at = st.at;
-    const bool ok = epc_eval(G, F, m, n, at, normY2, A, sP, Cb, red, X, en, dn);
-    if (threadIdx.x == 0) {   // (epc_eval ends with a block sum: every thread is past its reads of st)
-      if (ok) st.xmu = at;
+    const bool ok = s_ok != 0;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const unsigned long long t1 = ADMMQ_NOW();
+    if (ok)
+      for (int row = tid; row < m; row += kEpcThreads) tri_row_sums(Zt, m, n, row, cf, s0, s1, s2);
+    const unsigned long long t2 = ADMMQ_NOW();
+    block_sum3<kEpcThreads>(s0, s1, s2, red);
+    ev_ph[1] += t2 - t1;
+    ev_ph[2] += ADMMQ_NOW() - t2;
+    if (tid == 0) {
+      // e = ||Y||^2 - <F, X> - mu ||X||^2 with <F, X> = s, ||X||^2 = -s'; e' = mu s''
+      const double en = normY2 - s0 + at * s1, dn = at * s2;
       const int state = st.state;
       if (state == WARM) {
         if (ok) {
@@ -479,15 +873,40 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
         else {
           st.mu = at; st.e = en; st.de = dn;
           if (en < delta2) st.lo = at; else st.hi = at;
-          if (fabs(en - delta2) <= 16.0 * 0x1p-52 * normY2) st.state = FINAL;   // at the rounding floor of e
+          if (fabs(en - delta2) <= 16.0 * 0x1p-52 * normY2) st.state = DONE;   // at the rounding floor of e
         }
-      } else {
-        st.state = DONE;
       }
     }
-    __syncthreads();
   }
-  if (threadIdx.x == 0) { *mu_io = st.mu; if (info) *info = (st.have || st.mu == 0.0) ? 0 : 1; }
+  ADMMQ_EPC_STAMP(4);
+  if (ADMMQ_TRACE && tid == 0)
+    for (int q = 0; q < 3; ++q) g_epc_trace[13 + q] = ev_ph[q];
+  // X = (Z (T + mu I)^-1) Q^T at the returned mu (X first holds the forward pass, transposed)
+  if (tid == 0) s_ok = tri_ldl(dd, ee, n, st.mu, cf) ? 1 : 0;
+  __syncthreads();
+  const bool ok = s_ok != 0;
+  if (ok)
+    for (int row = tid; row < m; row += kEpcThreads) tri_row_solve(Zt, X, m, n, row, cf);   // (X: scratch here)
+  __syncthreads();
+  for (int r0 = 0; r0 < m; r0 += kEpcThreads / 16) {
+    const int row = r0 + (tid >> 4), c = tid & 15;
+    if (r0 + 4 * (tid >> 6) >= m) continue;
+    double y[kSpdPer];
+#pragma unroll
+    for (int q = 0; q < kSpdPer; ++q) {
+      const int j = c + 16 * q;
+      y[q] = (row < m && j < n) ? Zt[(size_t)j * m + row] : 0.0;
+    }
+    tri_apply_q(A, n, tau, -1, y);
+    if (row < m)
+#pragma unroll
+      for (int q = 0; q < kSpdPer; ++q) {
+        const int j = c + 16 * q;
+        if (j < n) X[(size_t)row * n + j] = ok ? y[q] : __builtin_nan("");
+      }
+  }
+  if (tid == 0) { *mu_io = st.mu; if (info) *info = ok && (st.have || st.mu == 0.0) ? 0 : 1; }
+  ADMMQ_EPC_STAMP(5);
 }
 
 }  // namespace admmq
@@ -512,6 +931,10 @@ int32_t admmq_debug_epc_evals(unsigned long long* out, int32_t reset) {
   return ADMMQ_OK;
 }
 
+int32_t admmq_debug_epc_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_epc_trace), sizeof(g_epc_trace)) == hipSuccess ? ADMMQ_OK : -1;
+}
+
 int32_t admmq_debug_spd_trace(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spd_trace), sizeof(g_spd_trace)) == hipSuccess ? ADMMQ_OK : -1;
 }
@@ -531,15 +954,15 @@ int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n
 }
 
 int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
-                         double* mu, double* X, int32_t* info, void* stream) {
-  if (!G || !F || !X || !mu || m <= 0 || n <= 0 || n > kSpdSmallMax || m > (1LL << 24))
+                         double* mu, double* X, double* work, int32_t* info, void* stream) {
+  if (!G || !F || !X || !mu || !work || m <= 0 || n <= 0 || n > kSpdSmallMax || m > (1LL << 24))
     return set_error(ADMMQ_ERR_ARG, "epc_step64: bad arguments (1 <= n <= 136)");
   const size_t lds = (size_t)n * spd_lda((int)n) * sizeof(double);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_epc_step64), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
   hipLaunchKernelGGL(k_epc_step64, dim3(1), dim3(kEpcThreads), lds, static_cast<hipStream_t>(stream), G, F, (int)m,
-                     (int)n, normY2, delta2, mu, X, info);
+                     (int)n, normY2, delta2, mu, X, work, info);
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "epc_step64: launch failed");
 }
 

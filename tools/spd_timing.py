@@ -48,3 +48,46 @@ if fn is not None and os.environ.get("ADMMQ_LIB", "").endswith("tracelib/libadmm
         ghz = (t[7] - t[4]) / ((t[3] - t[0]) * 10.0)   # shader clocks per ns
         print(f"trace n {n}: load G {(t[1] - t[0]) / 100:.1f} us, inverse {(t[2] - t[1]) / 100:.1f} us, "
               f"products {(t[3] - t[2]) / 100:.1f} us; shader clock {ghz:.2f} GHz")
+
+# the EPC step (k_epc_step64: tridiagonalisation + Z = F Q + the mu search + X), n = 134, m = 64
+fe = getattr(lib, "admmq_debug_epc_trace", None)
+n, m = 134, 64
+g = torch.Generator().manual_seed(5)
+B = torch.randn(n, n + 8, generator=g, dtype=torch.float64)
+G = (B @ B.T / (n + 8) + 1e-3 * torch.eye(n, dtype=torch.float64)).cuda()
+F = torch.randn(m, n, generator=g, dtype=torch.float64).cuda()
+X, W = torch.empty_like(F), torch.empty_like(F)
+ls = float(torch.sum(F * torch.linalg.solve(G, F.T).T))
+normY2, delta2 = ls * 1.5, ls * 0.5 * 2.5
+mu = torch.zeros((), dtype=torch.float64, device="cuda")
+st = _lib.stream_handle(F.device)
+call = lambda: lib.admmq_epc_step64(_lib.ptr(G), _lib.ptr(F), m, n, normY2, delta2, _lib.ptr(mu), _lib.ptr(X),  # noqa: E731
+                                    _lib.ptr(W), None, st)
+for warm in (False, True):
+    for _ in range(3):
+        if not warm:
+            mu.zero_()
+        call()
+    ev = (ctypes.c_ulonglong * 1)()
+    lib.admmq_debug_epc_evals(ev, 1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        if not warm:
+            mu.zero_()
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    lib.admmq_debug_epc_evals(ev, 1)
+    print(f"epc_step64 n {n} m {m} {'warm' if warm else 'cold'}: {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us per call, "
+          f"{ev[0] / 20:.1f} evaluations")
+    if fe is not None and os.environ.get("ADMMQ_LIB", "").endswith("tracelib/libadmmq.so"):
+        buf = (ctypes.c_ulonglong * 16)()
+        fe(buf)
+        t = [buf[k] for k in range(16)]
+        print(f"  trace: load G {(t[1] - t[0]) / 100:.1f} us, tridiagonal {(t[2] - t[1]) / 100:.1f} us, "
+              f"Z = F Q {(t[3] - t[2]) / 100:.1f} us, search {(t[4] - t[3]) / 100:.1f} us, X {(t[5] - t[4]) / 100:.1f} us")
+        print(f"  tridiagonal phases (sums over the steps): barrier 1 wait {t[8] / 100:.1f} us, matvec {t[9] / 100:.1f} us, "
+              f"barrier 2 wait {t[10] / 100:.1f} us, update {t[11] / 100:.1f} us, next reflector {t[12] / 100:.1f} us")
+        print(f"  search phases (sums): LDL coefficients {t[13] / 100:.1f} us, row sums {t[14] / 100:.1f} us, "
+              f"block sum {t[15] / 100:.1f} us")

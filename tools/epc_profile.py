@@ -53,7 +53,7 @@ lam, Us = pe.parafac_epc(W, R, als_maxiter=50, epc_maxiter=50)
 torch.cuda.synchronize()
 t = time.time() - t0
 _l.load().admmq_debug_epc_evals(ctypes.byref(_ev), 1)
-print(f"parafac_epc layer1.0.conv1 R={R}: {t:.2f} s; calls {calls}; EPC Cholesky evaluations {_ev.value}")
+print(f"parafac_epc layer1.0.conv1 R={R}: {t:.2f} s; calls {calls}; EPC error-equation evaluations {_ev.value}")
 G = torch.randn(R, 2 * R, device="cuda", dtype=torch.float64)
 G = G @ G.T
 F = torch.randn(64, R, device="cuda", dtype=torch.float64)
@@ -72,7 +72,7 @@ w, fs = pe.parafac(W, R, tol=1e-5, n_iter_max=50, normalize_factors=True)
 torch.cuda.synchronize()
 print(f"  parafac alone (50 its): {time.time() - t0:.2f} s")
 
-# the EPC step alone: Cholesky evaluations per call and device time per call, on the G / F of
+# the EPC step alone: error-equation evaluations per call and device time per call, on the G / F of
 # one mode of the factors just computed (warm start = the previous call's mu)
 import ctypes  # noqa: E402
 from admmq import _lib, panel  # noqa: E402

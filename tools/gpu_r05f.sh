@@ -3,7 +3,7 @@
 # line, then the kernel-trace stats of the default bench command for profiles/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-T=gpurun_out/r05f
+T=gpurun_out/${1:-r05f}
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf -s --timeout 300 --timeout-method thread > ${T}_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "C2 |C3 |parafac-epc|passed|failed|Error" ${T}_pytest.log | tail -20; [ $rc -ne 0 ] && exit $rc

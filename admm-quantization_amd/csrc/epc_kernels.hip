@@ -458,19 +458,20 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
         const double x = vb[min(j, m - 1)];
         vq[q] = j < m ? x : 0.0;
       }
+      // (the trailing block shrinks: row batches and column chunks past it are skipped by
+      // workgroup-uniform tests, not computed masked)
       double acc[kRowsPerGroup];
 #pragma unroll
       for (int b = 0; b < kRowsPerGroup; ++b) {
+        acc[b] = 0.0;
+        if (k + 1 + kGroups * b >= n) continue;   // uniform: no group has a row here
         const int r = k + 1 + g + kGroups * b;
         const double* Ar = A + min(r, n - 1) * lda + k + 1;
-        double a0 = Ar[min(c, m - 1)] * vq[0], a1 = Ar[min(c + 16, m - 1)] * vq[1], a2 = Ar[min(c + 32, m - 1)] * vq[2];
+        double a3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 3; q < kSpdPer; q += 3) {
-          a0 = fma(Ar[min(c + 16 * q, m - 1)], vq[q], a0);
-          if (q + 1 < kSpdPer) a1 = fma(Ar[min(c + 16 * (q + 1), m - 1)], vq[q + 1], a1);
-          if (q + 2 < kSpdPer) a2 = fma(Ar[min(c + 16 * (q + 2), m - 1)], vq[q + 2], a2);
-        }
-        acc[b] = (a0 + a1) + a2;
+        for (int q = 0; q < kSpdPer; ++q)
+          if (16 * q < m) a3[q % 3] = fma(Ar[min(c + 16 * q, m - 1)], vq[q], a3[q % 3]);
+        acc[b] = (a3[0] + a3[1]) + a3[2];
       }
 #pragma unroll
       for (int b = 0; b < kRowsPerGroup; ++b) acc[b] = sum16(acc[b]);
@@ -499,12 +500,13 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
     // of rows' loads before its stores (the compiler cannot tell the rows apart)
 #pragma unroll
     for (int b0 = 0; b0 < kRowsPerWave; b0 += kTriBatch) {
+      if (k + 1 + kWaves * b0 >= n) break;   // uniform: no wave has a row in this batch
       double a[kTriBatch][3];
 #pragma unroll
       for (int b = 0; b < kTriBatch; ++b) {
         const double* Ar = A + min(k + 1 + w + kWaves * (b0 + b), n - 1) * lda + k + 1;
 #pragma unroll
-        for (int h = 0; h < 3; ++h) a[b][h] = Ar[min(lane + 64 * h, m - 1)];
+        for (int h = 0; h < 3; ++h) a[b][h] = 64 * h < m ? Ar[min(lane + 64 * h, m - 1)] : 0.0;
       }
 #pragma unroll
       for (int b = 0; b < kTriBatch; ++b) {

@@ -353,6 +353,7 @@ __device__ unsigned long long g_epc_trace[16];   // [8 + k]: tridiagonalisation 
 // chain (a few microseconds), where an explicit (G + mu I)^-1 was O(n^3) on one workgroup;
 // the final X = (Z (T + mu)^-1) Q^T is one forward / backward pass and the reflectors applied
 // in reverse.
+constexpr int kEpcPad = 16 * kSpdPer;   // zeroed doubles after the matrix (unclamped reads past the last row)
 constexpr int kEpcThreads = 1024;   // (512: 256 VGPRs, but half the lanes on the rank-2 updates and two passes over
                                     // 64 rows in the reflector products: 0.79 vs 0.71 ms per step)
                                    // 128 VGPRs the compiler serialised them through one register pair)
@@ -417,6 +418,7 @@ __device__ __forceinline__ void tri_reflector(double* A, int n, int k, double* v
       row[j] = v;
     }
   }
+  for (int j = lane; j <= k; j += 64) row[j] = 0.0;   // v_k over the whole row (tri_apply_q)
   if (lane == 0) {
     dd[k] = dk;
     vb[0] = 1.0;
@@ -432,7 +434,7 @@ template <int NT>
 __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double* ee, double* tau, double* vb2,
                                             double* pb) {
   constexpr int kWaves = NT / 64, kGroups = NT / 16;
-  constexpr int kRowsPerWave = (kSpdSmallMax + kWaves - 1) / kWaves;      // update rows per wave
+  constexpr int kRowsPerWave = (kSpdSmallMax - 1 + kWaves - 2) / (kWaves - 1);   // update rows per wave (waves >= 1)
   constexpr int kRowsPerGroup = (kSpdSmallMax + kGroups - 1) / kGroups;   // matvec rows per 16-lane group
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lda = spd_lda(n);
   const int g = tid >> 4, c = tid & 15;
@@ -470,7 +472,7 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
         double a3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
         for (int q = 0; q < kSpdPer; ++q)
-          if (16 * q < m) a3[q % 3] = fma(Ar[min(c + 16 * q, m - 1)], vq[q], a3[q % 3]);
+          if (16 * q < m) a3[q % 3] = fma(Ar[c + 16 * q], vq[q], a3[q % 3]);   // (past m: finite values, or 0 past the LDS end, times vq = 0)
         acc[b] = (a3[0] + a3[1]) + a3[2];
       }
 #pragma unroll
@@ -496,21 +498,23 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
     const double K = 0.5 * t * sum64(pv);
 #pragma unroll
     for (int h = 0; h < 3; ++h) wj[h] -= K * vj[h];
-    // A22 -= v w^T + w v^T: rows r = k + 1 + w + kWaves b of this wave, lanes on columns; a batch
-    // of rows' loads before its stores (the compiler cannot tell the rows apart)
+    // A22 -= v w^T + w v^T, lanes on columns; wave 0 takes row k + 1 only (then forms the next
+    // reflector while the other waves finish: rows k + 1 + w + (kWaves - 1) b for w >= 1);
+    // a batch of rows' loads before its stores (the compiler cannot tell the rows apart)
+    const int rbase = k + 1 + w, rstep = w == 0 ? n : kWaves - 1;
 #pragma unroll
     for (int b0 = 0; b0 < kRowsPerWave; b0 += kTriBatch) {
-      if (k + 1 + kWaves * b0 >= n) break;   // uniform: no wave has a row in this batch
+      if (b0 > 0 && k + 2 + (kWaves - 1) * b0 >= n) break;   // uniform: no wave has a row in this batch
       double a[kTriBatch][3];
 #pragma unroll
       for (int b = 0; b < kTriBatch; ++b) {
-        const double* Ar = A + min(k + 1 + w + kWaves * (b0 + b), n - 1) * lda + k + 1;
+        const double* Ar = A + min(rbase + rstep * (b0 + b), n - 1) * lda + k + 1;
 #pragma unroll
-        for (int h = 0; h < 3; ++h) a[b][h] = 64 * h < m ? Ar[min(lane + 64 * h, m - 1)] : 0.0;
+        for (int h = 0; h < 3; ++h) a[b][h] = 64 * h < m ? Ar[lane + 64 * h] : 0.0;   // (lanes past m: not stored)
       }
 #pragma unroll
       for (int b = 0; b < kTriBatch; ++b) {
-        const int r = k + 1 + w + kWaves * (b0 + b);
+        const int r = rbase + rstep * (b0 + b);
         if (b0 + b < kRowsPerWave && r < n) {
           const double vi = vb[r - k - 1], wi = pb[r - k - 1] - K * vi;
           double* Ar = A + r * lda + k + 1;
@@ -544,27 +548,25 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
 }
 
 // One row of F -> F Q (dir = +1: H_0 first) or one row of Y -> Y Q^T (dir = -1: H_{n-3}
-// first), 16 lanes per row, lane c holding coordinates c + 16 q
+// first), 16 lanes per row, lane c holding coordinates c + 16 q. Row k of A holds v_k over
+// every column (zeros up to k, 1 at k + 1: tri_reflector), so a lane reads v_k[c + 16 q]
+// with an immediate offset and no clamp or select; only the chunk that crosses n masks (its
+// reads past the row's end are the next row's values, or 0 past the LDS allocation).
+// Issue-bound: ~60 wave-instructions per reflector and wave before, ~35 now.
 __device__ __forceinline__ void tri_apply_q(const double* A, int n, const double* tau, int dir, double (&f)[kSpdPer]) {
   const int c = threadIdx.x & 15, lda = spd_lda(n);
   for (int s = 0; s + 3 <= n; ++s) {
     const int k = dir > 0 ? s : n - 3 - s;
-    const double* v = A + k * lda;   // v_k at columns k + 1 ..
-    double vq[kSpdPer];
+    const double* v = A + k * lda + c;
+    double vq[kSpdPer], d3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < kSpdPer; ++q) {
-      const int j = c + 16 * q;
-      const double x = v[min(max(j, k + 1), n - 1)];   // (loaded unconditionally, then selected)
-      vq[q] = (j > k && j < n) ? x : 0.0;
+      double x = v[16 * q];
+      if (16 * q + 15 >= n) x = c + 16 * q < n ? x : 0.0;   // (uniform test: the crossing chunk only)
+      vq[q] = x;
+      d3[q % 3] = fma(f[q], x, d3[q % 3]);
     }
-    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
-#pragma unroll
-    for (int q = 0; q < kSpdPer; q += 3) {
-      d0 = fma(f[q], vq[q], d0);
-      if (q + 1 < kSpdPer) d1 = fma(f[q + 1], vq[q + 1], d1);
-      if (q + 2 < kSpdPer) d2 = fma(f[q + 2], vq[q + 2], d2);
-    }
-    const double d = sum16((d0 + d1) + d2) * tau[k];
+    const double d = sum16((d3[0] + d3[1]) + d3[2]) * tau[k];
 #pragma unroll
     for (int q = 0; q < kSpdPer; ++q) f[q] = fma(-d, vq[q], f[q]);
   }
@@ -763,6 +765,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
     A[i * lda + k] = v;
     if (i == k) tr += v;
   }
+  // the pad column and kEpcPad doubles past the matrix read as 0: the matvec's and the
+  // reflector products' unclamped reads past a row's end meet only finite values there
+  for (int i = tid; i < n; i += kEpcThreads) A[i * lda + n] = 0.0;
+  for (int e = tid; e < kEpcPad; e += kEpcThreads) A[n * lda + e] = 0.0;
   {
     double z1 = 0.0, z2 = 0.0;
     block_sum3<kEpcThreads>(tr, z1, z2, red);   // (its first barrier also publishes A)
@@ -959,7 +965,7 @@ int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n,
                          double* mu, double* X, double* work, int32_t* info, void* stream) {
   if (!G || !F || !X || !mu || !work || m <= 0 || n <= 0 || n > kSpdSmallMax || m > (1LL << 24))
     return set_error(ADMMQ_ERR_ARG, "epc_step64: bad arguments (1 <= n <= 136)");
-  const size_t lds = (size_t)n * spd_lda((int)n) * sizeof(double);
+  const size_t lds = ((size_t)n * spd_lda((int)n) + kEpcPad) * sizeof(double);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_epc_step64), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);

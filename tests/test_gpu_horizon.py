@@ -12,9 +12,9 @@ one run:
   * C2 (resnet18 layer1.0.conv1, every mode from the same seed-42 start, F and G from the
     oracle): the reference's iteration count, every result on a 4-bit grid (<= 16 levels),
     and the 999-iteration result's objective and grid step inside the reference's F11 band
-    or, where the CPU oracle's run of the same call lands outside it too (mode 2: F11's
-    1-ulp perturbations explore less than another summation order does), no farther outside
-    than the oracle;
+    (the step's band widened by one MSE candidate's spacing) or, where the CPU oracle's run
+    of the same call lands outside it too (mode 2: F11's 1-ulp perturbations explore less
+    than another summation order does), no farther outside than the oracle;
   * C2 as one ALS sweep (the three modes in sequence, the reference loop): the sweep's
     reconstruction errors (rec_error, quant_rec_error) inside the reference's F11 sweep band;
   * C3 (all 16 resnet18 3x3 convs batched, the bench's step): property checks on every
@@ -107,8 +107,13 @@ def test_c2_mode_call_at_bench_horizon(torch_dev, mode):
           f"oracle {so:.4e}, reference {min(ref['grid_step']):.4e} .. {max(ref['grid_step']):.4e}")
     # inside the band, or no farther outside it than the CPU restatement of the same call: F11's
     # 1-ulp proxy explores less than a different summation order does (mode 2: the oracle lands
-    # 0.7 % above the band, the device 0.06 %)
+    # 0.7 % above the band, the device 0.06 %). The grid step is one of the MSE search's 200
+    # candidates (t_c = mx (0.2 + c / 199), quantization.py:129-144): a run on another branch
+    # picks a neighbouring candidate, so its band is widened by one candidate's spacing at the
+    # top of the grid, the smallest relative spacing there is (1 / 238.8)
     assert _outside(og, lo, hi) <= _outside(oo, lo, hi), (og, oo, lo, hi)
+    cand = 1.0 / (0.2 * 199 + 199)
+    slo, shi = slo * (1 - cand), shi * (1 + cand)
     assert _outside(sg, slo, shi) <= _outside(so, slo, shi), (sg, so, slo, shi)
 
 

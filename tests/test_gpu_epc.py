@@ -133,13 +133,17 @@ def test_spd_solve64_vs_library(n, m):
     assert _rel(X, ref) < 1e-11, _rel(X, ref)
 
 
-@pytest.mark.parametrize("n,m,seed", [(134, 64, 1), (134, 9, 2), (7, 5, 3), (136, 64, 4)])
+@pytest.mark.parametrize("n,m,seed", [(134, 64, 1), (134, 9, 2), (7, 5, 3), (136, 64, 4), (1, 3, 5), (2, 7, 6),
+                                      (3, 70, 7), (40, 200, 8), (136, 1100, 9)])
 def test_epc_step64_vs_eigen_form(n, m, seed):
-    """The EPC mode update on the device (Newton on Cholesky factors of G + mu I, no
-    eigendecomposition) against the eigen form the oracle uses (oracle/epc_oracle.py:
-    eigh, mu by bisection to fp64 resolution, U = F V diag(1/(s + mu)) V^T) in float64 on
-    the CPU: mu and U within 1e-9, for targets needing mu > 0 (with and without a warm
-    start) and for one the least-squares step already meets (mu = 0)."""
+    """The EPC mode update on the device (csrc/epc_kernels.hip: G tridiagonalised once,
+    safeguarded Newton on tridiagonal L D L^T recurrences, no eigendecomposition) against
+    the eigen form the oracle uses (oracle/epc_oracle.py: eigh, mu by bisection to fp64
+    resolution, U = F V diag(1/(s + mu)) V^T) in float64 on the CPU: mu and U within 1e-9,
+    for targets needing mu > 0 (with and without a warm start) and for one the
+    least-squares step already meets (mu = 0). Sizes: no reflector (n = 1, 2), one
+    (n = 3), the LDS limit (136), several 64-row passes of the reflector products
+    (m = 70, 200) and more rows than threads (m = 1100)."""
     from admmq import panel
     g = torch.Generator().manual_seed(seed)
     B = torch.randn(n, n + 8, generator=g, dtype=torch.float64)

@@ -209,7 +209,7 @@ static bool layer64_ok(const admmq_cp_layer_f64& L) {
 }
 
 // Carve order: [jobs][units][split ids][partials]. Per layer: the mode's Gram(-Hadamard)
-// job, then its MTTKRP job (K chunks: enough units to fill the chip, chunks >= 512 rows).
+// job, then its MTTKRP job (K chunks: enough units to fill the chip, chunks >= 64 rows).
 static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* base, Cp64Plan& pl, std::string& err) {
   pl.jobs.clear(); pl.units.clear(); pl.split_ids.clear();
   for (int l = 0; l < n; ++l) {
@@ -247,7 +247,11 @@ static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* ba
     }
     f.out = L.F;
     const int tm = cdiv64(f.M, kC64BM), tn = cdiv64(f.N, kC64BN);
-    const int by_k = std::max(1, f.K / 512), by_fill = std::max(1, 512 / std::max(tm * tn, 1));
+    // chunks of >= 64 K (4 K-steps): a unit's time is its chain of K-steps, each waiting on
+    // the next step's global loads (the Khatri-Rao operand formed in flight), so the short
+    // reductions of the small EPC layers are cut as finely as the chip can hold (R = 134,
+    // (9, 64, 64): mode 0 24 -> 192 units, modes 1 / 2 3 -> 27)
+    const int by_k = std::max(1, f.K / 64), by_fill = std::max(1, 512 / std::max(tm * tn, 1));
     f.nsplit = std::max(1, std::min(by_k, by_fill));
     f.kchunk = cdiv64(cdiv64(f.K, f.nsplit), kC64BK) * kC64BK;
     f.nsplit = cdiv64(f.K, f.kchunk);

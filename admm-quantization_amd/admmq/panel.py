@@ -135,6 +135,26 @@ def epc_mu(c: torch.Tensor, s: torch.Tensor, normY2: float, delta2: float) -> to
     return mu
 
 
+def colnorm64(A: torch.Tensor, B: Optional[torch.Tensor] = None):
+    """cp_anc's normalisation of the other factors in one launch: ``A / max(||A[:, r]||, 1e-300)``
+    per column (and B likewise); new tensors, the inputs untouched (float64, contiguous, on
+    the device, the same number of columns)."""
+    for t in (A, B):
+        if t is not None and (t.dtype != torch.float64 or t.dim() != 2 or t.device.type != "cuda"):
+            raise ValueError("admmq.panel.colnorm64: float64 2-D device tensors")
+    if B is not None and B.shape[1] != A.shape[1]:
+        raise ValueError("admmq.panel.colnorm64: A and B need the same number of columns")
+    A = A.contiguous()
+    B = B.contiguous() if B is not None else None
+    oA = torch.empty_like(A)
+    oB = torch.empty_like(B) if B is not None else None
+    _lib.check(_lib.load().admmq_cp_colnorm64(_lib.ptr(A), A.shape[0], _lib.ptr(B) if B is not None else None,
+                                              B.shape[0] if B is not None else 0, A.shape[1], _lib.ptr(oA),
+                                              _lib.ptr(oB) if oB is not None else None,
+                                              _lib.stream_handle(A.device)), "cp_colnorm64")
+    return oA, oB
+
+
 SPD_SMALL_MAX = 136   # n of the one-workgroup fp64 solves (csrc/epc_kernels.hip: the matrix in LDS)
 
 

@@ -38,7 +38,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from .als import gram_mttkrp_f64
-from .panel import SPD_SMALL_MAX, epc_mu, epc_step64, spd_solve64
+from .panel import SPD_SMALL_MAX, colnorm64, epc_mu, epc_step64, spd_solve64
 
 _CHECK_EVERY = 8   # iterations between the host's reads of the device-side stop tests
 
@@ -155,12 +155,14 @@ def cp_anc(tensor: torch.Tensor, rank: int, delta: float, weights: Optional[torc
         snaps, lnorms = [], []
         for _ in range(min(_CHECK_EVERY, total - it)):
             for m in range(n):
-                # normalise the other factors, moving their column norms into factor m
-                for k in range(n):
-                    if k != m:
-                        nrm = torch.linalg.norm(fs[k], dim=0).clamp_min(1e-300)
-                        fs[k] = fs[k] / nrm
-                        fs[m] = fs[m] * nrm
+                # normalise the other factors, one launch for both (moving their column norms
+                # into factor m, as cp_anc does, would be dead work here: factor m is recomputed
+                # from F and G below before anything reads it)
+                o = [k for k in range(n) if k != m]
+                a, b = colnorm64(fs[o[0]], fs[o[1]] if len(o) > 1 else None)
+                fs[o[0]] = a
+                if len(o) > 1:
+                    fs[o[1]] = b
                 F, G = gram_mttkrp_f64(Y, fs, m)
                 fs[m] = _epc_update(G, F, normY2, delta2, mus[m])
             lnorms.append(torch.linalg.norm(torch.linalg.norm(fs[n - 1], dim=0)))

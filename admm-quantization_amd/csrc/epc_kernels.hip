@@ -917,6 +917,27 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   ADMMQ_EPC_STAMP(5);
 }
 
+// cp_anc's normalisation of the factors other than the updated one (one launch for both,
+// instead of a norm, a clamp and a division per factor): out = U / max(||U[:, r]||, 1e-300)
+// per column, a thread per column (coalesced across columns), the rows in order.
+struct CpColNorm { const double* src[2]; double* dst[2]; int rows[2]; };
+__global__ __launch_bounds__(256) void k_cp_colnorm(CpColNorm a, int R) {
+  const int r = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
+  if (r >= R) return;
+  const double* src = a.src[f];
+  double* dst = a.dst[f];
+  const int I = a.rows[f];
+  double acc = 0.0;
+#pragma unroll 8
+  for (int i = 0; i < I; ++i) {
+    const double v = src[(size_t)i * R + r];
+    acc = fma(v, v, acc);
+  }
+  const double nrm = fmax(sqrt(acc), 1e-300);
+#pragma unroll 8
+  for (int i = 0; i < I; ++i) dst[(size_t)i * R + r] = src[(size_t)i * R + r] / nrm;
+}
+
 }  // namespace admmq
 
 using namespace admmq;
@@ -937,6 +958,18 @@ int32_t admmq_debug_epc_evals(unsigned long long* out, int32_t reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_epc_evals), &z, sizeof(z)) != hipSuccess) return -1;
   }
   return ADMMQ_OK;
+}
+
+int32_t admmq_cp_colnorm64(const double* A, int64_t rowsA, const double* B, int64_t rowsB, int64_t R, double* outA,
+                           double* outB, void* stream) {
+  if (!A || !outA || rowsA < 1 || R < 1 || R > (1 << 24) || rowsA > (1 << 24) || (B && (!outB || rowsB < 1 || rowsB > (1 << 24))))
+    return set_error(ADMMQ_ERR_ARG, "cp_colnorm64: bad arguments");
+  CpColNorm a;
+  a.src[0] = A; a.dst[0] = outA; a.rows[0] = (int)rowsA;
+  a.src[1] = B; a.dst[1] = outB; a.rows[1] = B ? (int)rowsB : 0;
+  hipLaunchKernelGGL(k_cp_colnorm, dim3((unsigned)((R + 255) / 256), B ? 2u : 1u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a, (int)R);
+  return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "cp_colnorm64: launch failed");
 }
 
 int32_t admmq_debug_epc_trace(unsigned long long* out) {

@@ -308,6 +308,13 @@ int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n
 int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
                          double* mu, double* X, double* work, int32_t* info, void* stream);
 
+/* cp_anc's normalisation of the factors other than the one being updated
+ * (source/parafac_epc.py:61-74, musco cp_anc): outA = A / max(||A[:, r]||_2, 1e-300) per column r
+ * (A: rowsA x R row-major device doubles), and the same for B into outB when B is not NULL;
+ * one launch, no host synchronisation. */
+int32_t admmq_cp_colnorm64(const double* A, int64_t rowsA, const double* B, int64_t rowsB, int64_t R, double* outA,
+                           double* outB, void* stream);
+
 /* Library version (major*10000 + minor*100 + patch) and the last error text of this thread. */
 int32_t admmq_version(void);
 const char* admmq_last_error(void);

@@ -168,3 +168,25 @@ def test_epc_step64_vs_eigen_form(n, m, seed):
         else:
             assert abs(got - ref_mu) <= 1e-8 * ref_mu, (delta2, warm, got, ref_mu)
         assert _rel(X, ref_X) < 1e-9, (delta2, warm, _rel(X, ref_X))
+
+
+@pytest.mark.parametrize("rows,R", [((9, 64), 134), ((512, 512), 1141), ((7, None), 5)])
+def test_colnorm64_vs_torch(rows, R):
+    """The one-launch normalisation of cp_anc's other factors (admmq_cp_colnorm64) against
+    torch's U / norm(U, dim=0).clamp_min(1e-300): within 1e-15 relative (another summation
+    order of the column norms), a zero column left at zero, inputs untouched."""
+    from admmq import panel
+    g = torch.Generator().manual_seed(R)
+    A = torch.randn(rows[0], R, generator=g, dtype=torch.float64)
+    A[:, 0] = 0.0
+    B = torch.randn(rows[1], R, generator=g, dtype=torch.float64) if rows[1] else None
+    Ad, Bd = A.cuda(), (B.cuda() if B is not None else None)
+    oA, oB = panel.colnorm64(Ad, Bd)
+    for src, out in ((A, oA), (B, oB)):
+        if src is None:
+            assert out is None
+            continue
+        ref = src / torch.linalg.norm(src, dim=0).clamp_min(1e-300)
+        assert _rel(out, ref) < 1e-15, _rel(out, ref)
+    assert float(oA[:, 0].abs().max()) == 0.0
+    assert torch.equal(Ad.cpu(), A)

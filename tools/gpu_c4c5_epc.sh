@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 session x: C4 / C5 bench lines on the final tree, and the rocprofv3 kernel-trace
+# C4 / C5 bench lines, and the rocprofv3 kernel-trace
 # stats of the EPC initialiser on layer1.0.conv1 (tools/epc_profile.py).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-T=gpurun_out/r05x
+T=gpurun_out/${1:-c4c5_epc}
 export TMPDIR=/tmp
 for m in resnet50 llama7b; do
   timeout -k 10 400 python -u bench.py --model $m --steps 3 --warmup 1 --no-cpu-baseline > ${T}_bench_$m.json 2> ${T}_bench_$m.err || { tail ${T}_bench_$m.err; exit 5; }

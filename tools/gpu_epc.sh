@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 5 session i: EPC step phase trace, the EPC tests, the EPC profile.
+# The EPC step's phase trace (TRACE library), the EPC tests and the EPC profile.
+# Usage: tools/gpu_epc.sh TAG [trace]   (trace: the phase trace only)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 T=gpurun_out/${1:-r05i}

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 5 session f: the whole GPU suite on the committed tree, smoke, the default bench
-# line, then the kernel-trace stats of the default bench command for profiles/.
+# A round-end check on one GPU box: the whole GPU suite, smoke, the default bench
+# line, then the kernel-trace stats of the default bench command (outputs gpurun_out/TAG_*).
+# Usage: tools/gpu_round_check.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 T=gpurun_out/${1:-r05f}

@@ -795,8 +795,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   const double warm = *mu_io;
   // The search (a state machine in LDS, thread 0 deciding between evaluations; every branch
   // below uniform over the workgroup):
-  //   WARM   the warm start, when > 0: e < delta2 puts the root above it (mu > 0 for sure);
-  //   ZERO   mu = 0: e(0) >= delta2 means the LS step keeps the error (mu = 0, done);
+  //   WARM   the warm start, when > 0: e < delta2 puts the root above it (mu > 0 for sure),
+  //          otherwise Newton steps go down from it inside [0, warm];
+  //   ZERO   mu = 0 (first, without a warm start; else when a Newton step from above leaves
+  //          the bracket): e(0) >= delta2 means the LS step keeps the error (mu = 0, done);
   //   GROW   no upper end yet: from max(lo, trace / n 2^-20), doubling / Newton steps;
   //   NEWTON safeguarded Newton inside [lo, hi] until the step is below kEpcMuTol, the bracket
   //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
@@ -829,6 +831,7 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
         if (state == NEWTON) {
           if (!(st.hi - st.lo > kEpcMuTol * st.hi)) { st.state = DONE; break; }   // collapsed bracket
           double nx = st.de > 0.0 ? st.mu - (st.e - delta2) / st.de : -1.0;
+          if (!(nx > st.lo && nx < st.hi) && st.need0) { st.state = ZERO; continue; }   // below the bracket: is mu = 0 the answer?
           if (!(nx > st.lo && nx < st.hi)) nx = 0.5 * (st.lo + st.hi);
           if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = DONE; break; }   // converged
           st.at = nx;
@@ -860,15 +863,20 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
       const double en = normY2 - s0 + at * s1, dn = at * s2;
       const int state = st.state;
       if (state == WARM) {
+        // above the root: Newton down from the warm start, e(0) only if a step leaves the
+        // bracket (the LS step may keep the error: mu = 0); below it: grow
         if (ok) {
           st.mu = at; st.e = en; st.de = dn; st.have = 1;
           if (en < delta2) { st.lo = at; st.need0 = 0; }
           else st.hi = at;
         }
-        st.state = st.need0 ? ZERO : GROW;
+        st.state = !ok ? ZERO : (st.need0 ? NEWTON : GROW);
       } else if (state == ZERO) {
         if (ok && en >= delta2) { st.mu = 0.0; st.have = 0; st.state = DONE; }   // the LS step: mu = 0
-        else st.state = (st.have && st.hi < __builtin_huge_val()) ? NEWTON : GROW;
+        else {
+          st.need0 = 0;
+          st.state = (st.have && st.hi < __builtin_huge_val()) ? NEWTON : GROW;
+        }
       } else if (state == GROW) {
         if (!ok) st.lo = at;
         else {
@@ -880,7 +888,7 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
         if (!ok) st.lo = at;
         else {
           st.mu = at; st.e = en; st.de = dn;
-          if (en < delta2) st.lo = at; else st.hi = at;
+          if (en < delta2) { st.lo = at; st.need0 = 0; } else st.hi = at;   // (e increases with mu: e(0) <= e(lo))
           if (fabs(en - delta2) <= 16.0 * 0x1p-52 * normY2) st.state = DONE;   // at the rounding floor of e
         }
       }

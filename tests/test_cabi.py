@@ -166,3 +166,31 @@ def test_panel_entry_points_check_arguments(lib):
     assert lib.admmq_gram64(one, 3, one, 4, 8, 4, 4, one, one, 1 << 20, None) == ERR_ARG     # lda < p
     assert lib.admmq_gram64(one, 4, one, 4, 8, 4, 4, one, one, 8, None) == ERR_WS
     assert b"workspace" in lib.admmq_last_error()
+
+
+def test_epc_solves_refuse_bad_arguments(lib):
+    """The one-workgroup R x R solves and the column normalisation of the EPC initialiser
+    check their arguments on the host before any launch (include/admmq.h: 1 <= n <= 136,
+    non-NULL buffers); the Python wrappers refuse CPU or non-float64 tensors and n > 136,
+    and parafac_epc refuses a CPU tensor (no CPU path)."""
+    import torch
+    from admmq import panel
+    from admmq.parafac_epc import parafac_epc
+    p = ctypes.c_void_p(0x1000)
+    assert lib.admmq_spd_solve64(p, p, 4, 137, p, None, None) != 0          # n above the LDS limit
+    assert lib.admmq_spd_solve64(None, p, 4, 8, p, None, None) != 0         # no G
+    assert lib.admmq_epc_step64(p, p, 4, 137, 1.0, 0.5, p, p, p, None, None) != 0
+    assert lib.admmq_epc_step64(p, p, 4, 8, 1.0, 0.5, p, p, None, None, None) != 0   # no workspace
+    assert lib.admmq_cp_colnorm64(None, 4, None, 0, 8, p, None, None) != 0
+    assert lib.admmq_cp_colnorm64(p, 4, p, 3, 8, p, None, None) != 0        # B without its output
+    G = torch.eye(4, dtype=torch.float64)
+    F = torch.randn(3, 4, dtype=torch.float64)
+    with pytest.raises(ValueError):
+        panel.colnorm64(F)                                                 # a CPU tensor
+    with pytest.raises(ValueError):
+        panel.spd_solve64(G.float(), F)                                    # float32
+    with pytest.raises(ValueError):
+        panel.epc_step64(torch.eye(137, dtype=torch.float64), torch.randn(2, 137, dtype=torch.float64), 1.0, 0.5,
+                         torch.zeros((), dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        parafac_epc(torch.randn(4, 5, 6, dtype=torch.float64), 3)

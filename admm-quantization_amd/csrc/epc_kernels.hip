@@ -614,6 +614,69 @@ __device__ __forceinline__ bool tri_ldl(const double* __restrict__ dd, const dou
   return !bad;
 }
 
+// The same coefficients streamed for a running evaluation: producer A (one thread) runs the
+// D chain (one division and one fma per step) and writes L_{i-1} and 1 / D_i; producer B (a
+// thread of another wave) follows it with the derivative chains and the other four entries;
+// the row recurrences (tri_row_sums) follow B. Progress counters in LDS, advanced every
+// kTriChunk steps behind a workgroup release fence; waits are bounded (a stalled partner
+// leaves garbage, never a hang). Rows past n are zero (kTriPad), as in tri_ldl.
+__device__ __forceinline__ void tri_wait(const volatile int* prog, int need) {
+  for (int guard = 0; *prog < need && guard < (1 << 22); ++guard) __builtin_amdgcn_s_sleep(1);
+  // (a wave's LDS operations complete in order, so the loads below see what the producer
+  // stored before its release; only the compiler must not hoist them above the poll)
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void tri_publish(volatile int* prog, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  *prog = v;
+}
+__device__ __forceinline__ bool tri_ldl_a(const double* __restrict__ dd, const double* __restrict__ ee, int n,
+                                          double mu, double* __restrict__ P, volatile int* progA) {
+  double D = dd[0] + mu, L = 0.0;
+  double e = ee[0], an = dd[min(1, n - 1)] + mu;
+  bool bad = false;
+  for (int i = 0; i < n; ++i) {
+    bad |= !(D > 0.0) || !(D < __builtin_huge_val());
+    const double e_next = ee[min(i + 1, kSpdSmallMax - 1)], a_next = dd[min(i + 2, n - 1)] + mu;
+    const double gi = 1.0 / D;
+    double* Pi = P + kTriP * i;
+    Pi[0] = L;
+    Pi[3] = gi;
+    L = e * gi;
+    D = fma(-e * e, gi, an);
+    e = e_next;
+    an = a_next;
+    if ((i & (kTriChunk - 1)) == kTriChunk - 1) tri_publish(progA, i + 1);
+  }
+  for (int i = n; i < kTriPad; ++i) { P[kTriP * i] = 0.0; P[kTriP * i + 3] = 0.0; }
+  tri_publish(progA, kTriPad);
+  return !bad;
+}
+__device__ __forceinline__ void tri_ldl_b(const double* __restrict__ ee, int n, double* __restrict__ P,
+                                          const volatile int* progA, volatile int* progB) {
+  double D1 = 1.0, D2 = 0.0, L1 = 0.0, L2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    if ((i & (kTriChunk - 1)) == 0) tri_wait(progA, min(i + kTriChunk, kTriPad));
+    double* Pi = P + kTriP * i;
+    const double gi = Pi[3], g2 = gi * gi, e = ee[min(i, kSpdSmallMax - 1)];
+    Pi[1] = L1;
+    Pi[2] = L2;
+    Pi[4] = D1 * g2;
+    Pi[5] = D2 * g2 - 2.0 * D1 * D1 * g2 * gi;
+    L1 = -e * D1 * g2;
+    L2 = e * (2.0 * D1 * D1 * g2 * gi - D2 * g2);
+    D1 = fma(-e, L1, 1.0);
+    D2 = -e * L2;
+    if ((i & (kTriChunk - 1)) == kTriChunk - 1) tri_publish(progB, i + 1);
+  }
+  tri_wait(progA, kTriPad);
+  for (int i = n; i < kTriPad; ++i) {
+    double* Pi = P + kTriP * i;
+    Pi[1] = Pi[2] = Pi[4] = Pi[5] = 0.0;
+  }
+  tri_publish(progB, kTriPad);
+}
+
 // Block sums of three values (every thread's; the results in every thread)
 template <int NT>
 __device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* red) {
@@ -649,11 +712,12 @@ __device__ __forceinline__ TriCoef tri_coef(const double* P, int i) {
   return TriCoef{Pi[0], Pi[1], Pi[2], Pi[3], Pi[4], Pi[5]};
 }
 __device__ __forceinline__ void tri_row_sums(const double* __restrict__ Zt, int m, int n, int row, const double* P,
-                                             double& s0, double& s1, double& s2) {
+                                             const volatile int* progB, double& s0, double& s1, double& s2) {
   // every recurrence is one fma deep per step (the terms from the other chains formed off
   // it), and the sums alternate between two accumulators: a chained fp64 op costs ~30 clocks
   double u = 0.0, u1 = 0.0, u2 = 0.0;
   double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0}, a2[2] = {0.0, 0.0};
+  tri_wait(progB, min(kTriChunk, kTriPad));
   TriCoef cur = tri_coef(P, 0);
   auto steps = [&](const double (&zz)[kTriChunk], int i0) {   // (steps past n: P = 0, so no terms)
 #pragma unroll
@@ -683,6 +747,7 @@ __device__ __forceinline__ void tri_row_sums(const double* __restrict__ Zt, int 
   for (int i0 = 0; i0 < n; i0 += 2 * kTriChunk) {
 #pragma unroll
     for (int q = 0; q < kTriChunk; ++q) zb[q] = Zt[(size_t)min(i0 + kTriChunk + q, n - 1) * m + row];
+    tri_wait(progB, min(i0 + 2 * kTriChunk + 1, kTriPad));   // (a step reads the next step's coefficients)
     steps(za, i0);
 #pragma unroll
     for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(i0 + 2 * kTriChunk + q, n - 1) * m + row];
@@ -756,6 +821,7 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   __shared__ __attribute__((aligned(16))) double cf[kTriP * kTriPad];   // the tridiagonalisation's vb (2 x n) and pb, then the LDL coefficients
   __shared__ double red[3 * kEpcThreads / 64];
   __shared__ int s_ok;
+  __shared__ int s_prog[2];   // the streamed coefficients' progress (producers A, B)
   const int tid = threadIdx.x, lda = spd_lda(n);
   ADMMQ_EPC_STAMP(0);
   double tr = 0.0;   // trace(G) / n: the scale of the bracket's first step
@@ -841,25 +907,29 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
       }
       if (st.state != DONE) atomicAdd(&g_epc_evals, 1ull);
     }
-    if (tid == 0 && st.state != DONE) {   // the recurrence's coefficients there
-      const unsigned long long t0 = ADMMQ_NOW();
-      s_ok = tri_ldl(dd, ee, n, st.at, cf) ? 1 : 0;
-      ev_ph[0] += ADMMQ_NOW() - t0;
-    }
+    if (tid == 0) { s_prog[0] = 0; s_prog[1] = 0; }
     __syncthreads();   // (also: Zt written, before the first evaluation)
     if (st.state == DONE) break;
     const double at = st.at;
-    const bool ok = s_ok != 0;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     const unsigned long long t1 = ADMMQ_NOW();
-    if (ok)
-      for (int row = tid; row < m; row += kEpcThreads) tri_row_sums(Zt, m, n, row, cf, s0, s1, s2);
+    // the coefficients streamed by two producers (waves 1 and 2, lane 0) while the rows'
+    // recurrences (the other waves) follow them; ok (s_ok) is known after the block sum
+    if (tid == 64) {
+      s_ok = tri_ldl_a(dd, ee, n, at, cf, &s_prog[0]) ? 1 : 0;
+    } else if (tid == 128) {
+      tri_ldl_b(ee, n, cf, &s_prog[0], &s_prog[1]);
+    } else if (tid < 64 || tid >= 192) {
+      for (int row = tid < 64 ? tid : tid - 128; row < m; row += kEpcThreads - 128)
+        tri_row_sums(Zt, m, n, row, cf, &s_prog[1], s0, s1, s2);
+    }
     const unsigned long long t2 = ADMMQ_NOW();
     block_sum3<kEpcThreads>(s0, s1, s2, red);
     ev_ph[1] += t2 - t1;
     ev_ph[2] += ADMMQ_NOW() - t2;
     if (tid == 0) {
       // e = ||Y||^2 - <F, X> - mu ||X||^2 with <F, X> = s, ||X||^2 = -s'; e' = mu s''
+      const bool ok = s_ok != 0;
       const double en = normY2 - s0 + at * s1, dn = at * s2;
       const int state = st.state;
       if (state == WARM) {

@@ -870,10 +870,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
   //          a small |e - delta2| alone does not fix mu: the step decides).
   enum { WARM, ZERO, GROW, NEWTON, DONE };
-  struct St { double e, de, mu, lo, hi, at; int state, have, need0; };
+  struct St { double e, de, mu, lo, hi, at, pmu; int state, have, need0; };   // pmu: the mu of the coefficients in LDS
   __shared__ St st;
   if (tid == 0) {
-    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val();
+    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val(); st.pmu = __builtin_nan("");
     st.state = warm > 0.0 ? WARM : ZERO; st.have = 0; st.need0 = 1;
   }
   unsigned long long ev_ph[3] = {0ull, 0ull, 0ull};   // (TRACE: thread 0's LDL, row sums, block sum)
@@ -930,6 +930,7 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
     if (tid == 0) {
       // e = ||Y||^2 - <F, X> - mu ||X||^2 with <F, X> = s, ||X||^2 = -s'; e' = mu s''
       const bool ok = s_ok != 0;
+      st.pmu = ok ? at : __builtin_nan("");
       const double en = normY2 - s0 + at * s1, dn = at * s2;
       const int state = st.state;
       if (state == WARM) {
@@ -968,7 +969,8 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   if (ADMMQ_TRACE && tid == 0)
     for (int q = 0; q < 3; ++q) g_epc_trace[13 + q] = ev_ph[q];
   // X = (Z (T + mu I)^-1) Q^T at the returned mu (X first holds the forward pass, transposed)
-  if (tid == 0) s_ok = tri_ldl(dd, ee, n, st.mu, cf) ? 1 : 0;
+  if (tid == 0 && !(st.pmu == st.mu)) s_ok = tri_ldl(dd, ee, n, st.mu, cf) ? 1 : 0;   // (else: the last evaluation's, ok)
+  if (tid == 0 && st.pmu == st.mu) s_ok = 1;
   __syncthreads();
   const bool ok = s_ok != 0;
   if (ok)

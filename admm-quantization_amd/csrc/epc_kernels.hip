@@ -870,10 +870,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
   //          a small |e - delta2| alone does not fix mu: the step decides).
   enum { WARM, ZERO, GROW, NEWTON, DONE };
-  struct St { double e, de, mu, lo, hi, at, pmu; int state, have, need0; };   // pmu: the mu of the coefficients in LDS
+  struct St { double e, de, mu, lo, hi, at, pmu, q0; int state, have, need0; };   // pmu: the mu of the coefficients in LDS
   __shared__ St st;
   if (tid == 0) {
-    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val(); st.pmu = __builtin_nan("");
+    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val(); st.pmu = __builtin_nan(""); st.q0 = 0.0;
     st.state = warm > 0.0 ? WARM : ZERO; st.have = 0; st.need0 = 1;
   }
   unsigned long long ev_ph[3] = {0ull, 0ull, 0ull};   // (TRACE: thread 0's LDL, row sums, block sum)
@@ -884,7 +884,7 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
         if (state == WARM) { st.at = warm; break; }
         if (state == ZERO) { st.at = 0.0; break; }
         if (state == GROW) {
-          double at = st.have ? 2.0 * fmax(st.mu, st.lo) : (tr > 0.0 ? tr * 0x1p-20 : 1e-300);
+          double at = st.have ? 2.0 * fmax(st.mu, st.lo) : (st.q0 > 0.0 ? st.q0 : (tr > 0.0 ? tr * 0x1p-20 : 1e-300));
           if (st.have && st.de > 0.0) {   // a Newton step from below (lands above the root: e convex near it)
             const double nx = st.mu - (st.e - delta2) / st.de;
             if (nx > st.mu && nx < at) at = nx;
@@ -945,6 +945,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
       } else if (state == ZERO) {
         if (ok && en >= delta2) { st.mu = 0.0; st.have = 0; st.state = DONE; }   // the LS step: mu = 0
         else {
+          // a cold start's first step from the model e(mu) ~ e(0) + mu^2 <X0, X0 G^-1> near 0
+          // (e' = 2 mu <X, X A^-1>, and s'' / 2 = <X, X A^-1>): it lands at or below the root
+          // where <X, X A^-1> falls with mu, so the growth continues from there
+          if (ok && s2 > 0.0) st.q0 = sqrt((delta2 - en) / (0.5 * s2));
           st.need0 = 0;
           st.state = (st.have && st.hi < __builtin_huge_val()) ? NEWTON : GROW;
         }

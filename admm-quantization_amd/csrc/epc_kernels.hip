@@ -547,6 +547,145 @@ __device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double
   __syncthreads();
 }
 
+// The tridiagonalisation with the matrix in registers. Wave w holds rows r = w + 16 t (t < 9)
+// of the full symmetric matrix, lane l columns l + 64 h (h < 3): 27 doubles per lane. The
+// rank-2 update is then register-only VALU work (no LDS round trip per element: the LDS form
+// spent ~2 us per column step moving A22 through the LDS pipes), and LDS carries only the
+// vectors: v, the matvec's per-wave partial column sums (p = A v = A^T v, each wave summing
+// its own rows, the 16 partials added in wave order by one thread per column, in the free rows
+// of A past the current step), p itself. The reflector of step k + 1 is formed from registers
+// by the wave owning row k + 1, right after its update. Reflector rows go to A in LDS as
+// tri_apply_q reads them (zeros up to k, 1, v). Three workgroup barriers per step.
+constexpr int kRegRows = (kSpdSmallMax + 15) / 16;   // rows per wave (9)
+
+template <int NT>
+__device__ __forceinline__ void tridiag_regs(const double* __restrict__ G, int n, double* A, double* dd, double* ee,
+                                             double* tau, double* vb2, double* pb) {
+  static_assert(NT == 1024, "16 waves x kRegRows rows");
+  constexpr int kW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lda = spd_lda(n);
+  double a[kRegRows][3];
+#pragma unroll
+  for (int t = 0; t < kRegRows; ++t) {
+    const int r = w + kW * t;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int j = lane + 64 * h;
+      a[t][h] = (r < n && j < n) ? G[(size_t)r * n + j] : 0.0;
+    }
+  }
+  auto store_row = [&](int t, int r) {   // this wave's row a[t] (wave-uniform t) into row r of A
+#pragma unroll
+    for (int tt = 0; tt < kRegRows; ++tt)
+      if (tt == t)
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int j = lane + 64 * h;
+          if (j < n) A[r * lda + j] = a[tt][h];
+        }
+  };
+  if (n >= 3 && w == 0) {
+    store_row(0, 0);
+    asm volatile("" ::: "memory");
+    tri_reflector(A, n, 0, vb2, tau, dd, ee);
+  }
+  unsigned long long ph[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tp = ADMMQ_NOW();
+#define ADMMQ_TRI_PH(q)                               \
+  if (ADMMQ_TRACE) {                                  \
+    const unsigned long long tn_ = ADMMQ_NOW();       \
+    ph[q] += tn_ - tp;                                \
+    tp = tn_;                                         \
+  }
+  for (int k = 0; k + 3 <= n; ++k) {
+    const int m = n - k - 1;
+    const double* vb = vb2 + (k & 1) * kSpdSmallMax;
+    double* part = A + (k + 1) * lda;   // rows k + 1 .. (and the pad) are free until their reflectors
+    __syncthreads();   // v_k, tau_k visible
+    ADMMQ_TRI_PH(0);
+    const double t_ = tau[k];
+    {   // this wave's partial column sums of A22 v over its rows r >= k + 1
+      double ps[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < kRegRows; ++t) {
+        const int r = w + kW * t;
+        if (r >= k + 1 && r < n) {
+          const double vr = vb[r - k - 1];
+#pragma unroll
+          for (int h = 0; h < 3; ++h) ps[h] = fma(a[t][h], vr, ps[h]);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int j = lane + 64 * h;
+        if (j >= k + 1 && j < n) part[w * m + (j - k - 1)] = ps[h];
+      }
+    }
+    ADMMQ_TRI_PH(1);
+    __syncthreads();
+    if (tid < m) {   // p = tau A22 v: the 16 waves' partials in wave order
+      double sacc = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < kW; ++ww) sacc += part[ww * m + tid];
+      pb[tid] = t_ * sacc;
+    }
+    __syncthreads();
+    ADMMQ_TRI_PH(2);
+    double vj[3], wj[3], pv = 0.0;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int i = lane + 64 * h - k - 1;
+      const int ic = min(max(i, 0), m - 1);
+      const double xv = vb[ic], xw = pb[ic];
+      vj[h] = (i >= 0 && i < m) ? xv : 0.0;
+      wj[h] = (i >= 0 && i < m) ? xw : 0.0;
+      pv = fma(vj[h], wj[h], pv);
+    }
+    const double K = 0.5 * t_ * sum64(pv);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) wj[h] = fma(-K, vj[h], wj[h]);
+#pragma unroll
+    for (int t = 0; t < kRegRows; ++t) {   // A22 -= v w^T + w v^T on this wave's rows
+      const int r = w + kW * t;
+      if (r >= k + 1 && r < n) {
+        const double vr = vb[r - k - 1], wr = fma(-K, vr, pb[r - k - 1]);
+#pragma unroll
+        for (int h = 0; h < 3; ++h) a[t][h] = fma(-vr, wj[h], fma(-wr, vj[h], a[t][h]));
+      }
+    }
+    ADMMQ_TRI_PH(3);
+    if (k + 4 <= n && w == (k + 1) % kW) {   // the owner of row k + 1: the next reflector, from
+      store_row((k + 1) / kW, k + 1);         // its row put where the reflector will be stored
+      asm volatile("" ::: "memory");
+      tri_reflector(A, n, k + 1, vb2 + ((k + 1) & 1) * kSpdSmallMax, tau, dd, ee);
+    }
+    ADMMQ_TRI_PH(4);
+  }
+#undef ADMMQ_TRI_PH
+  if (ADMMQ_TRACE && tid == 0)
+    for (int q = 0; q < 5; ++q) g_epc_trace[8 + q] = ph[q];
+  // the last diagonal / off-diagonal entries, from their owners' registers (via rows n - 2,
+  // n - 1 of A, free: no reflector goes there)
+  __syncthreads();
+  if (n >= 2 && w == (n - 2) % kW) store_row((n - 2) / kW, n - 2);
+  if (w == (n - 1) % kW) store_row((n - 1) / kW, n - 1);
+  __syncthreads();
+  if (tid == 0) {
+    if (n >= 2) {
+      dd[n - 2] = A[(n - 2) * lda + n - 2];
+      ee[n - 2] = A[(n - 2) * lda + n - 1];
+    }
+    dd[n - 1] = A[(n - 1) * lda + n - 1];
+  }
+  // rows n - 2, n - 1 and the pad held partials: zero them (tri_apply_q's crossing chunk
+  // reads past the last reflector row) and so did the pad column of rows 1 .. n - 3; row 0's
+  // was never written: all of them to 0 (tri_apply_q's unclamped reads meet only zeros there)
+  __syncthreads();
+  const int r0 = max(n - 2, 0);
+  for (int e = tid; e < (n - r0) * lda + kEpcPad; e += NT) A[r0 * lda + e] = 0.0;
+  for (int i = tid; i < r0; i += NT) A[i * lda + n] = 0.0;
+  __syncthreads();
+}
+
 // One row of F -> F Q (dir = +1: H_0 first) or one row of Y -> Y Q^T (dir = -1: H_{n-3}
 // first), 16 lanes per row, lane c holding coordinates c + 16 q. Row k of A holds v_k over
 // every column (zeros up to k, 1 at k + 1: tri_reflector), so a lane reads v_k[c + 16 q]
@@ -825,23 +964,14 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   const int tid = threadIdx.x, lda = spd_lda(n);
   ADMMQ_EPC_STAMP(0);
   double tr = 0.0;   // trace(G) / n: the scale of the bracket's first step
-  for (int e = tid; e < n * n; e += kEpcThreads) {
-    const int i = e / n, k = e - i * n;
-    const double v = G[e];
-    A[i * lda + k] = v;
-    if (i == k) tr += v;
-  }
-  // the pad column and kEpcPad doubles past the matrix read as 0: the matvec's and the
-  // reflector products' unclamped reads past a row's end meet only finite values there
-  for (int i = tid; i < n; i += kEpcThreads) A[i * lda + n] = 0.0;
-  for (int e = tid; e < kEpcPad; e += kEpcThreads) A[n * lda + e] = 0.0;
+  for (int i = tid; i < n; i += kEpcThreads) tr += G[(size_t)i * n + i];
   {
     double z1 = 0.0, z2 = 0.0;
-    block_sum3<kEpcThreads>(tr, z1, z2, red);   // (its first barrier also publishes A)
+    block_sum3<kEpcThreads>(tr, z1, z2, red);
   }
   tr /= (double)n;
   ADMMQ_EPC_STAMP(1);
-  tridiag_lds<kEpcThreads>(A, n, dd, ee, tau, cf, cf + 2 * kSpdSmallMax);
+  tridiag_regs<kEpcThreads>(G, n, A, dd, ee, tau, cf, cf + 2 * kSpdSmallMax);
   ADMMQ_EPC_STAMP(2);
   // Z = F Q, stored transposed (Zt[i * m + row]: the row recurrences read it coalesced)
   for (int r0 = 0; r0 < m; r0 += kEpcThreads / 16) {

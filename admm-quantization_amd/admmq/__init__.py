@@ -14,7 +14,7 @@ Drop-in replacements for KamikaziZen/admm-quantization's hot path:
 Compute runs in libadmmq.so (hand-written HIP for gfx950) through a C ABI
 (include/admmq.h); there is no CPU fallback.
 """
-from .admm import admm_iteration, admm_iteration_batched, init_factors, squared_relative_diff  # noqa: F401
+from .admm import admm_iteration, admm_iteration_batched, init_factors, init_factors_many, squared_relative_diff  # noqa: F401
 from .quantization import quantize_tensor, quantize_tensor_mse, min_max_quantize, quantize_batched  # noqa: F401
 from .utils import unfold  # noqa: F401
 

@@ -157,6 +157,12 @@ def load() -> ctypes.CDLL:
         "admmq_gram64": (I32, [P, I64, P, I64, I64, I64, I64, P, P, S, P]),
         "admmq_epc_mu": (I32, [P, P, I64, ctypes.c_double, ctypes.c_double, P, P]),
         "admmq_cp_colnorm64": (I32, [P, I64, P, I64, I64, P, P, P]),
+        "admmq_solve64_workspace_size": (S, [I64, I64]),
+        "admmq_debug_s64_evals": (I32, [P, I32]),
+        "admmq_spd_solve64_ws": (I32, [P, P, I64, I64, ctypes.c_double, P, P, P, S, P]),
+        "admmq_epc_begin64": (I32, [P, P, I64, I64, ctypes.c_double, ctypes.c_double, P, P, P, S, P]),
+        "admmq_epc_rounds64": (I32, [P, P, I64, I64, P, I32, P, P, S, P]),
+        "admmq_epc_end64": (I32, [I64, I64, P, P, P, S, P]),
         "admmq_version": (I32, []),
         "admmq_last_error": (ctypes.c_char_p, []),
     }

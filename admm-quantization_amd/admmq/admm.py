@@ -30,7 +30,7 @@ from . import _lib
 from .quantization import _scheme_code
 from .utils import unfold
 
-__all__ = ["admm_iteration", "admm_iteration_batched", "init_factors", "squared_relative_diff"]
+__all__ = ["admm_iteration", "admm_iteration_batched", "init_factors", "init_factors_many", "squared_relative_diff"]
 
 
 def squared_relative_diff(X: torch.Tensor, Y: torch.Tensor) -> float:
@@ -72,6 +72,24 @@ def init_factors(tensor: torch.Tensor, rank: int, init: str = "random", device=N
     else:
         raise NotImplementedError(init)
     return factors
+
+
+def init_factors_many(tensors: Sequence[torch.Tensor], ranks: Sequence[int], init: str = "random", device=None,
+                      seed=None) -> List[List[torch.Tensor]]:
+    """``init_factors`` for every layer of a model (the reference runs scripts/factorize.py once
+    per layer, each calling source/admm.py:21-48): the same factors as one call per layer. With
+    ``parafac-epc`` the layers' initialisers run concurrently, one HIP stream each
+    (``admmq.parafac_epc.parafac_epc_many``): a model's initialisation then takes about as long
+    as its slowest layers instead of the sum."""
+    if len(tensors) != len(ranks):
+        raise ValueError("init_factors_many: one rank per tensor")
+    if init != "parafac-epc" or not tensors:
+        return [init_factors(t, rank=r, init=init, device=device, seed=seed) for t, r in zip(tensors, ranks)]
+    from .parafac_epc import parafac_epc_many
+    dev = torch.device(device) if device is not None else tensors[0].device
+    res = parafac_epc_many([t.to(dev) for t in tensors], [int(r) for r in ranks], init="random", als_maxiter=50,
+                           epc_maxiter=50)
+    return [[f.to(device=dev, dtype=torch.float32) for f in us] for _, us in res]
 
 
 def _problem(H, U, F, G, HT_out=None, X_out=None):

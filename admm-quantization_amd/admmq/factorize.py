@@ -29,7 +29,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib, synthetic
-from .admm import admm_iteration_batched, init_factors
+from .admm import admm_iteration_batched, init_factors_many
 from .als import gram_mttkrp, gram_mttkrp_batched, rel_error_batched  # noqa: F401
 from .quantization import quantize_batched
 
@@ -175,10 +175,11 @@ def factorize_layers(weights: Sequence[torch.Tensor], ranks: Sequence[int], max_
     scripts/factorize.py:249-253, 301-305) plus the sweep's wall time and ADMM
     factor-iterations (see :func:`sweep_records`)."""
     runs = []
+    if initial_factors is None:   # every layer's init at once (parafac-epc: one stream per layer)
+        initial_factors = init_factors_many(weights, ranks, init=init, device=weights[0].device if weights else None,
+                                            seed=seed)
     for i, (W, R) in enumerate(zip(weights, ranks)):
-        fs = initial_factors[i] if initial_factors is not None else init_factors(W, rank=R, init=init, device=W.device,
-                                                                                 seed=seed)
-        fs = [f.contiguous().clone() for f in fs]
+        fs = [f.to(W.device).contiguous().clone() for f in initial_factors[i]]
         run = LayerRun(names[i] if names else f"layer{i}", W, R, fs)
         if init != "random":   # scripts/factorize.py:192-204: record the starting point
             q = quantize_batched(fs, bits, qscheme, num_attempts=num_attempts)

@@ -8,7 +8,8 @@ fallback: the HIP library must be loaded.
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Tuple
+from collections import OrderedDict
+from typing import Optional, Tuple
 
 import torch
 
@@ -21,8 +22,8 @@ from . import _lib
 # streams from racing on the same slots and counters. A workspace is allocated on its own
 # stream, so when it is grown the caching allocator reuses the old block only for later work
 # of that same stream - never while another stream's kernel may still read it.
-_WS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
-_GWS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+_WS: "OrderedDict[Tuple[torch.device, int], torch.Tensor]" = OrderedDict()
+_GWS: "OrderedDict[Tuple[torch.device, int], torch.Tensor]" = OrderedDict()
 
 
 def _key(dev: torch.device) -> Tuple[torch.device, int]:
@@ -33,12 +34,7 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     """The partials / arrival counters of the panel kernels, per (device, current stream),
     grown on demand and zeroed when (re)allocated (the counters must start at a multiple of
     the group size)."""
-    k = _key(dev)
-    ws = _WS.get(k)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
-        _WS[k] = ws
-    return ws
+    return _cached(_WS, dev, nbytes, zero=True)
 
 
 def _check_x(X: torch.Tensor) -> torch.Tensor:
@@ -113,11 +109,7 @@ def gram(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -
     C = out if out is not None else torch.empty(p, q, dtype=torch.float64, device=A.device)
     lib = _lib.load()
     nb = lib.admmq_gram64_workspace_size(m, p, q)
-    k = _key(A.device)
-    ws = _GWS.get(k)
-    if ws is None or ws.numel() < nb:
-        ws = torch.empty(max(int(nb), 256), dtype=torch.uint8, device=A.device)
-        _GWS[k] = ws
+    ws = _cached(_GWS, A.device, nb, zero=False)
     _lib.check(lib.admmq_gram64(_lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), m, p, q, _lib.ptr(C), _lib.ptr(ws),
                                 ws.numel(), _lib.stream_handle(A.device)), "gram64")
     return C
@@ -156,41 +148,135 @@ def colnorm64(A: torch.Tensor, B: Optional[torch.Tensor] = None):
 
 
 SPD_SMALL_MAX = 136   # n of the one-workgroup fp64 solves (csrc/epc_kernels.hip: the matrix in LDS)
+EPC_FIRST_ROUNDS = 3   # blocked EPC step: evaluation rounds queued before the first read of its done flag
+EPC_NEXT_ROUNDS = 2    # ... and between later reads
+
+_SWS: "OrderedDict[Tuple[torch.device, int], torch.Tensor]" = OrderedDict()   # blocked-solve workspaces
+_CACHE_MAX = 64   # workspaces kept per cache (least recently used dropped; see _cached)
 
 
-def spd_solve64(G: torch.Tensor, F: torch.Tensor) -> torch.Tensor:
-    """``F G^-1`` (m x n float64) for SPD ``G`` (n x n, n <= SPD_SMALL_MAX) on the device: the
-    CP-ALS update ``torch.linalg.solve(G, F.T).T`` of tensorly ``parafac`` (one workgroup,
-    Cholesky in LDS, no host synchronisation; a non-SPD G gives NaN rows instead of raising)."""
+def _cached(cache, dev: torch.device, nbytes: int, zero: bool) -> torch.Tensor:
+    """The workspace of the current stream (grown on demand). At most _CACHE_MAX streams keep one:
+    the least recently used is released to the caching allocator, which reuses a block only for
+    later work of the stream it was allocated on, so a kernel still queued there is safe."""
+    k = _key(dev)
+    ws = cache.get(k)
+    if ws is None or ws.numel() < nbytes:
+        ws = (torch.zeros if zero else torch.empty)(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        cache[k] = ws
+    cache.move_to_end(k)
+    while len(cache) > _CACHE_MAX:
+        cache.popitem(last=False)
+    return ws
+
+
+def _check_solve(G: torch.Tensor, F: torch.Tensor, what: str):
     n = G.shape[0]
     if G.dtype != torch.float64 or F.dtype != torch.float64 or G.shape != (n, n) or F.dim() != 2 or F.shape[1] != n:
-        raise ValueError("admmq.panel.spd_solve64: G (n x n) and F (m x n) must be float64")
+        raise ValueError(f"admmq.panel.{what}: G (n x n) and F (m x n) must be float64")
+    if G.device.type != "cuda" or F.device != G.device:
+        raise RuntimeError(f"admmq.panel.{what}: G and F must be on one ROCm GPU (no CPU implementation)")
+    return G.contiguous(), F.contiguous()
+
+
+def _info_ptr(info: Optional[torch.Tensor]):
+    if info is None:
+        return None
+    if info.dtype != torch.int32 or info.numel() != 1 or info.device.type != "cuda":
+        raise ValueError("admmq.panel: info must be a one-element int32 device tensor")
+    return _lib.ptr(info)
+
+
+def spd_solve64(G: torch.Tensor, F: torch.Tensor, info: Optional[torch.Tensor] = None,
+                rel_shift: float = 0.0) -> torch.Tensor:
+    """``F (G + rel_shift (tr G / n) I)^-1`` (m x n float64) for SPD ``G`` on the device: the CP-ALS
+    update ``torch.linalg.solve(G, F.T).T`` of tensorly ``parafac``, with no host synchronisation.
+    n <= SPD_SMALL_MAX: one workgroup, an unpivoted blocked Gauss-Jordan inverse in LDS; larger n:
+    the blocked fp64 Cholesky L L^T, L^-1 and X = (F L^-T) L^-1 on fp64 MFMA
+    (``csrc/solve64.hip``). A G that is not numerically positive definite sets ``info`` (a
+    one-element int32 device tensor) to 1 and leaves X undefined; without ``info`` it goes
+    unnoticed, so the drivers always pass one (``admmq.parafac_epc`` retries such an update
+    with a small relative shift)."""
+    G, F = _check_solve(G, F, "spd_solve64")
+    m, n = F.shape
+    X = torch.empty(F.shape, dtype=torch.float64, device=F.device)
+    if m == 0:
+        return X
+    lib = _lib.load()
+    ws = None
+    nb = 0
     if n > SPD_SMALL_MAX:
-        raise ValueError(f"admmq.panel.spd_solve64: n = {n} > {SPD_SMALL_MAX}")
-    G, F = G.contiguous(), F.contiguous()
-    X = torch.full(F.shape, float("nan"), dtype=torch.float64, device=F.device)
-    _lib.check(_lib.load().admmq_spd_solve64(_lib.ptr(G), _lib.ptr(F), F.shape[0], n, _lib.ptr(X), None,
-                                             _lib.stream_handle(F.device)), "spd_solve64")
+        nb = lib.admmq_solve64_workspace_size(m, n)
+        ws = _cached(_SWS, F.device, nb, zero=False)
+    _lib.check(lib.admmq_spd_solve64_ws(_lib.ptr(G), _lib.ptr(F), m, n, float(rel_shift), _lib.ptr(X), _info_ptr(info),
+                                        _lib.ptr(ws) if ws is not None else None, ws.numel() if ws is not None else 0,
+                                        _lib.stream_handle(F.device)), "spd_solve64")
     return X
 
 
-def epc_step64(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor) -> torch.Tensor:
+def epc_step64(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor,
+               info: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One EPC mode update of musco ``cp_anc`` on the device: ``F (G + mu I)^-1`` with ``mu >= 0``
-    the root of the error equation (``csrc/epc_kernels.hip``: G tridiagonalised once, then
-    safeguarded Newton steps on tridiagonal LDL^T recurrences, no eigendecomposition). ``mu`` is a 0-dim float64 device tensor: the warm
-    start in, the root out (updated in place). n <= SPD_SMALL_MAX; no host synchronisation."""
+    the root of the error equation. ``mu`` is a 0-dim float64 device tensor: the warm start in,
+    the root out (updated in place). n <= SPD_SMALL_MAX: one launch (``csrc/epc_kernels.hip``: G
+    tridiagonalised once, then safeguarded Newton steps on tridiagonal L D L^T recurrences; no
+    host synchronisation); larger n: the blocked step (``epc_step64_gen``), driven to completion
+    here. ``info`` (one-element int32 device tensor): 0, or 1 when no G + mu I on the search
+    bracket was positive definite or the search did not converge."""
+    if G.shape[0] > SPD_SMALL_MAX:
+        gen = epc_step64_gen(G, F, normY2, delta2, mu, info)
+        try:
+            ev = next(gen)
+            while True:
+                ev.synchronize()
+                ev = gen.send(None)
+        except StopIteration as stop:
+            return stop.value
+    G, F = _check_solve(G, F, "epc_step64")
     n = G.shape[0]
-    if G.dtype != torch.float64 or F.dtype != torch.float64 or G.shape != (n, n) or F.dim() != 2 or F.shape[1] != n:
-        raise ValueError("admmq.panel.epc_step64: G (n x n) and F (m x n) must be float64")
-    if n > SPD_SMALL_MAX:
-        raise ValueError(f"admmq.panel.epc_step64: n = {n} > {SPD_SMALL_MAX}")
     if mu.dtype != torch.float64 or mu.numel() != 1 or mu.device != F.device:
         raise ValueError("admmq.panel.epc_step64: mu must be a float64 scalar tensor on F's device")
-    G, F = G.contiguous(), F.contiguous()
     X = torch.empty(F.shape, dtype=torch.float64, device=F.device)
     work = torch.empty(F.shape, dtype=torch.float64, device=F.device)
     _lib.check(_lib.load().admmq_epc_step64(_lib.ptr(G), _lib.ptr(F), F.shape[0], n, float(normY2), float(delta2),
-                                            _lib.ptr(mu), _lib.ptr(X), _lib.ptr(work), None,
+                                            _lib.ptr(mu), _lib.ptr(X), _lib.ptr(work), _info_ptr(info),
                                             _lib.stream_handle(F.device)),
                "epc_step64")
+    return X
+
+
+def epc_step64_gen(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: float, mu: torch.Tensor,
+                   info: Optional[torch.Tensor] = None):
+    """The blocked EPC step for any n (``csrc/solve64.hip``) as a generator: it queues evaluation
+    rounds (each a Cholesky of G + mu I at the search's next mu and the Newton update, all on the
+    device) and yields a ``torch.cuda.Event`` whenever it needs the done flag on the host
+    (``EPC_FIRST_ROUNDS`` rounds, then ``EPC_NEXT_ROUNDS`` per read); resume it once the event has
+    completed. Returns X = F (G + mu I)^-1; ``mu`` updated in place, ``info`` as ``epc_step64``.
+    ``admmq.parafac_epc`` drives several of these at once, one layer per stream."""
+    G, F = _check_solve(G, F, "epc_step64")
+    m, n = F.shape
+    if mu.dtype != torch.float64 or mu.numel() != 1 or mu.device != F.device:
+        raise ValueError("admmq.panel.epc_step64: mu must be a float64 scalar tensor on F's device")
+    lib = _lib.load()
+    dev = F.device
+    X = torch.empty(F.shape, dtype=torch.float64, device=dev)
+    nb = lib.admmq_solve64_workspace_size(m, n)
+    ws = _cached(_SWS, dev, nb, zero=False)
+    done = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = _lib.stream_handle(dev)
+    _lib.check(lib.admmq_epc_begin64(_lib.ptr(G), _lib.ptr(F), m, n, float(normY2), float(delta2), _lib.ptr(mu),
+                                     _lib.ptr(X), _lib.ptr(ws), ws.numel(), st), "epc_begin64")
+    rounds, total = EPC_FIRST_ROUNDS, 0
+    while total < 96:
+        _lib.check(lib.admmq_epc_rounds64(_lib.ptr(G), _lib.ptr(F), m, n, _lib.ptr(X), rounds, _lib.ptr(done),
+                                          _lib.ptr(ws), ws.numel(), st), "epc_rounds64")
+        total += rounds
+        host = done.to("cpu", non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        yield ev
+        if int(host[0]):
+            break
+        rounds = EPC_NEXT_ROUNDS
+    _lib.check(lib.admmq_epc_end64(m, n, _lib.ptr(mu), _info_ptr(info), _lib.ptr(ws), ws.numel(), st), "epc_end64")
     return X

@@ -221,6 +221,7 @@ void launch_rho(const ProbDesc* d, int nprob, hipStream_t s);
 void launch_pack(const ProbDesc* d, int nprob, int maxIp, int maxld, hipStream_t s);
 void launch_fill_a64(const ProbDesc* d, int nprob, int maxldm, hipStream_t s);
 void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
+void launch_spd_linv(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s);
 void launch_thin_solve(const ProbDesc* d, const ThinLoopUnit* units, int nunits, int nr, int maxld, int slot, int iter,
                        float eps, int ncand, hipStream_t s);
 void launch_gemm(const ProbDesc* d, const GemmTile* tiles, int ntiles_wide, int ntiles_small, int ntiles_big,

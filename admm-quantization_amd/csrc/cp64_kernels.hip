@@ -18,32 +18,9 @@
 
 #include "../../include/admmq.h"
 #include "admmq_internal.h"
+#include "cp64.h"
 
 namespace admmq {
-
-typedef double f64x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kC64BM = 64, kC64BN = 64, kC64BK = 16, kC64NT = 256;
-constexpr int kC64LD = kC64BM + 8;   // LDS row stride (doubles): the 4 k rows of a fragment read on distinct banks
-constexpr int kC64PA = kC64BK * kC64BM / kC64NT;   // A elements per thread per K-step
-constexpr int kC64PB = kC64BK * kC64BN / kC64NT;   // B elements per thread per K-step
-
-struct Cp64Job {
-  int kind;             // 0 MTTKRP, 1 Gram(-Hadamard)
-  int M, N, K;          // output rows / cols, reduction length (MTTKRP)
-  int nsplit, kchunk;   // MTTKRP: K chunks and their length (multiple of kC64BK)
-  int K2;               // MTTKRP: Khatri-Rao inner extent (1: one other factor, 2-way)
-  int afast;            // A side staged along rows (rows contiguous in memory)
-  int R, Kx, Ky;        // Gram: rank, rows of X, rows of Y (0: no Hadamard factor)
-  int pad_;
-  long long sm, s1, s2; // MTTKRP: Y_(n)[a, k] = W[a sm + (k / K2) s1 + (k % K2) s2]
-  const double* W;
-  const double* X;      // MTTKRP: KR outer factor ((K / K2) x N); Gram: first factor (Kx x R)
-  const double* Y;      // MTTKRP: KR inner factor (K2 x N) or nullptr; Gram: second factor or nullptr
-  double* part;         // MTTKRP: [nsplit][M][N] partial planes (nsplit > 1)
-  double* out;          // MTTKRP: F (M x N); Gram: G (R x R)
-};
-struct Cp64Unit { int job, tm, tn, ks; };
 
 __device__ __forceinline__ double c64_opA(const Cp64Job& j, int which, int m, int k) {
   if (j.kind == 0) {
@@ -54,7 +31,10 @@ __device__ __forceinline__ double c64_opA(const Cp64Job& j, int which, int m, in
 }
 __device__ __forceinline__ double c64_opB(const Cp64Job& j, int which, int k, int n) {
   if (j.kind == 0) {
-    if (j.K2 == 1) return j.X[(long long)k * j.N + n];
+    if (j.K2 == 1) {   // (also the plain GEMM: B row-major k x n, or transposed; tri masks a triangle)
+      const double v = j.bt ? j.X[(long long)n * j.ldb + k] : j.X[(long long)k * j.ldb + n];
+      return j.tri == 0 ? v : ((j.tri == 1 ? k <= n : k >= n) ? v : 0.0);
+    }
     const int kq = k / j.K2, kr = k - kq * j.K2;
     return j.X[(long long)kq * j.N + n] * j.Y[(long long)kr * j.N + n];
   }
@@ -68,7 +48,7 @@ __device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, in
                                          double (*sB)[kC64BK * kC64LD]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const bool afast = j.afast != 0;
+  const bool afast = j.afast != 0, bfast = j.bt != 0;   // bfast: B staged along k (B^T rows contiguous)
   double ra[kC64PA], rb[kC64PB];
   auto load = [&](int k0) {
 #pragma unroll
@@ -81,7 +61,7 @@ __device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, in
 #pragma unroll
     for (int e = 0; e < kC64PB; ++e) {
       const int x = tid + kC64NT * e;
-      const int c = x % kC64BN, kk = x / kC64BN;
+      const int c = bfast ? x / kC64BK : x % kC64BN, kk = bfast ? x % kC64BK : x / kC64BN;
       const int n = n0 + c, k = k0 + kk;
       rb[e] = (n < Ncols && k < ke) ? c64_opB(j, which, k, n) : 0.0;
     }
@@ -96,7 +76,8 @@ __device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, in
 #pragma unroll
     for (int e = 0; e < kC64PB; ++e) {
       const int x = tid + kC64NT * e;
-      sB[buf][(x / kC64BN) * kC64LD + x % kC64BN] = rb[e];
+      const int c = bfast ? x / kC64BK : x % kC64BN, kk = bfast ? x % kC64BK : x / kC64BN;
+      sB[buf][kk * kC64LD + c] = rb[e];
     }
   };
   if (kb >= ke) return;
@@ -140,12 +121,16 @@ __global__ __launch_bounds__(kC64NT) void k_cp64(const Cp64Job* __restrict__ job
   __shared__ __attribute__((aligned(16))) double sB[2][kC64BK * kC64LD];
   const Cp64Unit u = units[blockIdx.x];
   const Cp64Job& j = jobs[u.job];
+  if (j.gate && *j.gate) return;   // a round of the blocked EPC step after its search is done
   const int m0 = u.tm * kC64BM, n0 = u.tn * kC64BN;
   f64x4 acc[2][2];
   c64_zero(acc);
   double* dst;
   if (j.kind == 0) {
-    const int kb = u.ks * j.kchunk, ke = min(j.K, kb + j.kchunk);
+    // the chunk, clipped to the rows of B a triangular operand can have nonzero (tri 1: k <= n,
+    // so k < n0 + 64; tri 2: k >= n0); an empty chunk leaves its partial plane zero
+    const int kb = max(u.ks * j.kchunk, j.tri == 2 ? n0 : 0);
+    const int ke = min(min(j.K, u.ks * j.kchunk + j.kchunk), j.tri == 1 ? n0 + kC64BN : j.K);
     c64_core(j, 0, m0, n0, kb, ke, j.M, j.N, acc, sA, sB);
     dst = j.nsplit > 1 ? j.part + (size_t)u.ks * j.M * j.N : j.out;
   } else {
@@ -180,6 +165,7 @@ __global__ __launch_bounds__(kC64NT) void k_cp64(const Cp64Job* __restrict__ job
 // MTTKRP split-K: F = sum over chunks s (in order) of part[s]. grid.y = job.
 __global__ __launch_bounds__(256) void k_cp64_reduce(const Cp64Job* __restrict__ jobs, const int* __restrict__ ids) {
   const Cp64Job& j = jobs[ids[blockIdx.y]];
+  if (j.gate && *j.gate) return;
   const size_t n = (size_t)j.M * j.N;
   for (size_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (size_t)gridDim.x * 256) {
     double s = j.part[e];
@@ -193,13 +179,6 @@ __global__ __launch_bounds__(256) void k_cp64_reduce(const Cp64Job* __restrict__
 
 static inline size_t al64(size_t v) { return (v + 255) / 256 * 256; }
 static inline int cdiv64(long long a, long long b) { return (int)((a + b - 1) / b); }
-
-struct Cp64Plan {
-  std::vector<Cp64Job> jobs;
-  std::vector<Cp64Unit> units;
-  std::vector<int> split_ids;
-  size_t bytes = 0;
-};
 
 static bool layer64_ok(const admmq_cp_layer_f64& L) {
   if (!L.W || (L.ndim != 2 && L.ndim != 3) || L.R < 1) return false;
@@ -221,7 +200,7 @@ static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* ba
     if (base && (!L.F || !L.G)) { err = "cp64 layer: F / G output missing"; return ADMMQ_ERR_ARG; }
     Cp64Job g;
     std::memset(&g, 0, sizeof(g));
-    g.kind = 1; g.R = R; g.M = g.N = R; g.afast = 1;
+    g.kind = 1; g.R = R; g.M = g.N = R; g.afast = 1; g.ldb = R;
     int o[2], no = 0;
     for (int d = 0; d < L.ndim; ++d)
       if (d != mode) o[no++] = d;
@@ -229,12 +208,14 @@ static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* ba
     if (no == 2) { g.Y = L.factors[o[1]]; g.Ky = L.dims[o[1]]; }
     g.out = L.G;
     const int gid = (int)pl.jobs.size();
-    pl.jobs.push_back(g);
+    g.unit0 = (int)pl.units.size();
     for (int a = 0; a < cdiv64(R, kC64BM); ++a)
       for (int b = 0; b < cdiv64(R, kC64BN); ++b) pl.units.push_back({gid, a, b, 0});
+    g.nunits = (int)pl.units.size() - g.unit0;
+    pl.jobs.push_back(g);
     Cp64Job f;
     std::memset(&f, 0, sizeof(f));
-    f.kind = 0; f.N = R; f.W = L.W; f.M = L.dims[mode];
+    f.kind = 0; f.N = R; f.ldb = R; f.W = L.W; f.M = L.dims[mode];
     const long long JK = (long long)J * Kd;
     if (L.ndim == 3) {   // k runs over the other two modes in their order (torch unfold / Khatri-Rao order)
       if (mode == 0) { f.K = J * Kd; f.K2 = Kd; f.sm = JK; f.s1 = Kd; f.s2 = 1; f.X = L.factors[1]; f.Y = L.factors[2]; }
@@ -257,10 +238,12 @@ static int plan_cp64(const admmq_cp_layer_f64* layers, int n, int mode, void* ba
     f.nsplit = cdiv64(f.K, f.kchunk);
     const int fid = (int)pl.jobs.size();
     if (f.nsplit > 1) pl.split_ids.push_back(fid);
-    pl.jobs.push_back(f);
+    f.unit0 = (int)pl.units.size();
     for (int ks = 0; ks < f.nsplit; ++ks)
       for (int a = 0; a < tm; ++a)
         for (int b = 0; b < tn; ++b) pl.units.push_back({fid, a, b, ks});
+    f.nunits = (int)pl.units.size() - f.unit0;
+    pl.jobs.push_back(f);
   }
   size_t off = 0;
   char* b = static_cast<char*>(base);
@@ -302,6 +285,83 @@ static int run_cp64(const Cp64Plan& pl, void* base, size_t wsb, hipStream_t s, s
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { err = std::string("cp64 launch: ") + hipGetErrorString(e); return ADMMQ_ERR_HIP; }
   return ADMMQ_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// Plain fp64 GEMMs (the blocked R x R solves of solve64.hip)
+
+void cp64_plan_gemm(Cp64Plan& pl, const double* A, long long lda, const double* B, long long ldb, int bt, int tri,
+                    double* C, int M, int N, int K, const int* gate) {
+  Cp64Job f;
+  std::memset(&f, 0, sizeof(f));
+  f.kind = 0; f.M = M; f.N = N; f.K = K; f.K2 = 1;
+  f.W = A; f.sm = lda; f.s1 = 1; f.s2 = 0;
+  f.X = B; f.ldb = ldb; f.bt = bt; f.tri = tri;
+  f.out = C; f.gate = gate;
+  const int tm = cdiv64(M, kC64BM), tn = cdiv64(N, kC64BN);
+  // K chunks of >= 64 to bring the units to ~512 (2 per CU): a 64 x 64 tile's K chain is
+  // latency-bound at these sizes (k_cp64's staging waits on each step's loads)
+  const int by_k = std::max(1, K / 64), by_fill = std::max(1, 512 / std::max(tm * tn, 1));
+  f.nsplit = std::max(1, std::min(by_k, by_fill));
+  f.kchunk = cdiv64(cdiv64(K, f.nsplit), kC64BK) * kC64BK;
+  f.nsplit = cdiv64(K, f.kchunk);
+  const int fid = (int)pl.jobs.size();
+  if (f.nsplit > 1) pl.split_ids.push_back(fid);
+  f.unit0 = (int)pl.units.size();
+  for (int ks = 0; ks < f.nsplit; ++ks)
+    for (int a = 0; a < tm; ++a)
+      for (int b = 0; b < tn; ++b) pl.units.push_back({fid, a, b, ks});
+  f.nunits = (int)pl.units.size() - f.unit0;
+  pl.jobs.push_back(f);
+}
+
+// Carve order: [jobs][units][split ids][partials] (as plan_cp64).
+size_t cp64_carve(Cp64Plan& pl, void* base) {
+  size_t off = 0;
+  char* b = static_cast<char*>(base);
+  auto take = [&](size_t nbytes) -> char* { char* p = b ? b + off : nullptr; off += al64(nbytes); return p; };
+  take(pl.jobs.size() * sizeof(Cp64Job));
+  take(pl.units.size() * sizeof(Cp64Unit));
+  take(pl.split_ids.size() * sizeof(int) + 4);
+  for (auto& j : pl.jobs)
+    if (j.kind == 0 && j.nsplit > 1) j.part = reinterpret_cast<double*>(take((size_t)j.nsplit * j.M * j.N * 8));
+  pl.bytes = off + 256;
+  return pl.bytes;
+}
+
+struct Cp64Tables { Cp64Job* jobs; Cp64Unit* units; int* ids; };
+static Cp64Tables cp64_tables(const Cp64Plan& pl, void* base) {
+  size_t off = 0;
+  char* b = static_cast<char*>(base);
+  auto take = [&](size_t nbytes) -> char* { char* p = b + off; off += al64(nbytes); return p; };
+  Cp64Tables t;
+  t.jobs = reinterpret_cast<Cp64Job*>(take(pl.jobs.size() * sizeof(Cp64Job)));
+  t.units = reinterpret_cast<Cp64Unit*>(take(pl.units.size() * sizeof(Cp64Unit)));
+  t.ids = reinterpret_cast<int*>(take(pl.split_ids.size() * sizeof(int) + 4));
+  return t;
+}
+
+int cp64_upload(const Cp64Plan& pl, void* base, hipStream_t s) {
+  const Cp64Tables t = cp64_tables(pl, base);
+  if (upload_async(t.jobs, pl.jobs.data(), pl.jobs.size() * sizeof(Cp64Job), s) != ADMMQ_OK ||
+      upload_async(t.units, pl.units.data(), pl.units.size() * sizeof(Cp64Unit), s) != ADMMQ_OK ||
+      upload_async(t.ids, pl.split_ids.data(), pl.split_ids.size() * sizeof(int), s) != ADMMQ_OK)
+    return ADMMQ_ERR_HIP;
+  return ADMMQ_OK;
+}
+
+int cp64_launch_job(const Cp64Plan& pl, void* base, int job, hipStream_t s) {
+  const Cp64Tables t = cp64_tables(pl, base);
+  const Cp64Job& j = pl.jobs[job];
+  if (j.nunits > 0) hipLaunchKernelGGL(k_cp64, dim3((unsigned)j.nunits), dim3(kC64NT), 0, s, t.jobs, t.units + j.unit0);
+  if (j.nsplit > 1) {
+    int pos = 0;
+    while (pl.split_ids[pos] != job) ++pos;
+    const size_t mn = (size_t)j.M * j.N;
+    const int nb = (int)std::min<size_t>(256, (mn + 255) / 256);
+    hipLaunchKernelGGL(k_cp64_reduce, dim3(nb, 1), dim3(256), 0, s, t.jobs, t.ids + pos);
+  }
+  return hipGetLastError() == hipSuccess ? ADMMQ_OK : ADMMQ_ERR_HIP;
 }
 
 }  // namespace admmq

@@ -6,6 +6,7 @@
 
 #include "../../include/admmq.h"
 #include "admmq_internal.h"
+#include "epc_search.h"
 
 namespace admmq {
 
@@ -64,10 +65,11 @@ __global__ __launch_bounds__(256) void k_epc_mu(const double* __restrict__ c, co
 //   k_epc_step64    X = F (G + mu I)^-1 with mu >= 0 the root of the EPC error equation
 //                   e(mu) = ||Y||^2 - <F, X> - mu ||X||^2 = delta^2 (the eigen form's
 //                   ||Y||^2 - sum_j c_j (s_j + 2 mu) / (s_j + mu)^2 with G = V diag(s) V^T,
-//                   c_j = |F v_j|^2), found by Newton steps on e, e'(mu) = 2 mu ||X L^-T||^2,
-//                   safeguarded by the bracket [lo, hi] (bisection / doubling), each from a
-//                   fresh Cholesky of G + mu I; mu = 0 when e(0) >= delta^2 already (the LS
-//                   step keeps the error).
+//                   c_j = |F v_j|^2), found by Newton steps on e, e'(mu) = 2 mu <X, X (G + mu I)^-1>,
+//                   safeguarded by the bracket [lo, hi] (bisection / doubling; epc_search.h),
+//                   each evaluation on tridiagonal L D L^T recurrences after one Householder
+//                   reduction of G per call (below); mu = 0 when e(0) >= delta^2 already (the
+//                   LS step keeps the error).
 //
 // The inverse (G + shift I)^-1 in LDS by blocked Gauss-Jordan without pivoting (G + shift I
 // SPD: positive pivots), then the right-hand sides as one dense product X = F (G + shift I)^-1.
@@ -302,14 +304,23 @@ __device__ __forceinline__ double spd_block_sum(double v, double* red) {
   return t;
 }
 
+// rel_shift > 0: X = F (G + rel_shift (trace(G) / n) I)^-1 (the regularised retry of a CP-ALS
+// update whose G was not numerically positive definite; admmq.parafac_epc)
 __global__ __launch_bounds__(kSpdThreads) void k_spd_solve64(const double* __restrict__ G, const double* __restrict__ F,
-                                                             int m, int n, double* __restrict__ X,
+                                                             int m, int n, double rel_shift, double* __restrict__ X,
                                                              int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) double A[];
   __shared__ double sP[kGJ * kGJ];
   ADMMQ_SPD_STAMP(0);
   __shared__ double Cb[kSpdSmallMax * kGJ];
-  const bool ok = spd_inverse_lds<kSpdThreads>(G, n, 0.0, A, sP, Cb);
+  double shift = 0.0;
+  if (rel_shift > 0.0) {
+    __shared__ double red[kSpdThreads / 64];
+    double t = 0.0;
+    for (int i = threadIdx.x; i < n; i += kSpdThreads) t += G[(size_t)i * n + i];
+    shift = rel_shift * spd_block_sum<kSpdThreads>(t, red) / (double)n;
+  }
+  const bool ok = spd_inverse_lds<kSpdThreads>(G, n, shift, A, sP, Cb);
   ADMMQ_SPD_STAMP(2);
   if (!ok) {
     if (threadIdx.x == 0 && info) *info = 1;
@@ -354,9 +365,9 @@ __device__ unsigned long long g_epc_trace[16];   // [8 + k]: tridiagonalisation 
 // the final X = (Z (T + mu)^-1) Q^T is one forward / backward pass and the reflectors applied
 // in reverse.
 constexpr int kEpcPad = 16 * kSpdPer;   // zeroed doubles after the matrix (unclamped reads past the last row)
-constexpr int kEpcThreads = 1024;   // (512: 256 VGPRs, but half the lanes on the rank-2 updates and two passes over
-                                    // 64 rows in the reflector products: 0.79 vs 0.71 ms per step)
-                                   // 128 VGPRs the compiler serialised them through one register pair)
+// 1024 threads: at 512 (256 VGPRs) half the lanes sat out the rank-2 updates and the reflector
+// products took two passes over 64 rows (0.79 vs 0.71 ms per step)
+constexpr int kEpcThreads = 1024;
 
 // Householder tridiagonalisation of the symmetric A (LDS, n x n, lda = n + 1) in place:
 // dd (diagonal), ee (off-diagonal), tau_k and v_k (v_k[k + 1] = 1, stored in row k from
@@ -428,134 +439,6 @@ __device__ __forceinline__ void tri_reflector(double* A, int n, int k, double* v
   }
 }
 
-constexpr int kTriBatch = 3;   // update rows loaded before their stores
-
-template <int NT>
-__device__ __forceinline__ void tridiag_lds(double* A, int n, double* dd, double* ee, double* tau, double* vb2,
-                                            double* pb) {
-  constexpr int kWaves = NT / 64, kGroups = NT / 16;
-  constexpr int kRowsPerWave = (kSpdSmallMax - 1 + kWaves - 2) / (kWaves - 1);   // update rows per wave (waves >= 1)
-  constexpr int kRowsPerGroup = (kSpdSmallMax + kGroups - 1) / kGroups;   // matvec rows per 16-lane group
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lda = spd_lda(n);
-  const int g = tid >> 4, c = tid & 15;
-  if (n >= 3 && w == 0) tri_reflector(A, n, 0, vb2, tau, dd, ee);
-  unsigned long long ph[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tp = ADMMQ_NOW();
-#define ADMMQ_TRI_PH(k)                               \
-  if (ADMMQ_TRACE) {                                  \
-    const unsigned long long tn_ = ADMMQ_NOW();       \
-    ph[k] += tn_ - tp;                                \
-    tp = tn_;                                         \
-  }
-  for (int k = 0; k + 3 <= n; ++k) {
-    const int m = n - k - 1;
-    const double* vb = vb2 + (k & 1) * kSpdSmallMax;
-    __syncthreads();   // v_k, tau_k (and step k - 1's update) visible
-    ADMMQ_TRI_PH(0);
-    const double t = tau[k];
-    {   // p = tau A22 v: the group's rows' partial sums first, then their 16-lane sums together
-      double vq[kSpdPer];
-#pragma unroll
-      for (int q = 0; q < kSpdPer; ++q) {
-        const int j = c + 16 * q;
-        const double x = vb[min(j, m - 1)];
-        vq[q] = j < m ? x : 0.0;
-      }
-      // (the trailing block shrinks: row batches and column chunks past it are skipped by
-      // workgroup-uniform tests, not computed masked)
-      double acc[kRowsPerGroup];
-#pragma unroll
-      for (int b = 0; b < kRowsPerGroup; ++b) {
-        acc[b] = 0.0;
-        if (k + 1 + kGroups * b >= n) continue;   // uniform: no group has a row here
-        const int r = k + 1 + g + kGroups * b;
-        const double* Ar = A + min(r, n - 1) * lda + k + 1;
-        double a3[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < kSpdPer; ++q)
-          if (16 * q < m) a3[q % 3] = fma(Ar[c + 16 * q], vq[q], a3[q % 3]);   // (past m: finite values, or 0 past the LDS end, times vq = 0)
-        acc[b] = (a3[0] + a3[1]) + a3[2];
-      }
-#pragma unroll
-      for (int b = 0; b < kRowsPerGroup; ++b) acc[b] = sum16(acc[b]);
-#pragma unroll
-      for (int b = 0; b < kRowsPerGroup; ++b) {
-        const int r = k + 1 + g + kGroups * b;
-        if (c == 0 && r < n) pb[r - k - 1] = t * acc[b];
-      }
-    }
-    ADMMQ_TRI_PH(1);
-    __syncthreads();
-    ADMMQ_TRI_PH(2);
-    double vj[3], wj[3], pv = 0.0;
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {
-      const int i = lane + 64 * h;
-      const double xv = vb[min(i, m - 1)], xw = pb[min(i, m - 1)];
-      vj[h] = i < m ? xv : 0.0;
-      wj[h] = i < m ? xw : 0.0;
-      pv += vj[h] * wj[h];
-    }
-    const double K = 0.5 * t * sum64(pv);
-#pragma unroll
-    for (int h = 0; h < 3; ++h) wj[h] -= K * vj[h];
-    // A22 -= v w^T + w v^T, lanes on columns; wave 0 takes row k + 1 only (then forms the next
-    // reflector while the other waves finish: rows k + 1 + w + (kWaves - 1) b for w >= 1);
-    // a batch of rows' loads before its stores (the compiler cannot tell the rows apart)
-    const int rbase = k + 1 + w, rstep = w == 0 ? n : kWaves - 1;
-#pragma unroll
-    for (int b0 = 0; b0 < kRowsPerWave; b0 += kTriBatch) {
-      if (b0 > 0 && k + 2 + (kWaves - 1) * b0 >= n) break;   // uniform: no wave has a row in this batch
-      double a[kTriBatch][3];
-#pragma unroll
-      for (int b = 0; b < kTriBatch; ++b) {
-        const double* Ar = A + min(rbase + rstep * (b0 + b), n - 1) * lda + k + 1;
-#pragma unroll
-        for (int h = 0; h < 3; ++h) a[b][h] = 64 * h < m ? Ar[lane + 64 * h] : 0.0;   // (lanes past m: not stored)
-      }
-#pragma unroll
-      for (int b = 0; b < kTriBatch; ++b) {
-        const int r = rbase + rstep * (b0 + b);
-        if (b0 + b < kRowsPerWave && r < n) {
-          const double vi = vb[r - k - 1], wi = pb[r - k - 1] - K * vi;
-          double* Ar = A + r * lda + k + 1;
-#pragma unroll
-          for (int h = 0; h < 3; ++h) {
-            const int i = lane + 64 * h;
-            if (i < m) Ar[i] = fma(-vi, wj[h], fma(-wi, vj[h], a[b][h]));
-          }
-        }
-      }
-    }
-    ADMMQ_TRI_PH(3);
-    if (w == 0 && k + 4 <= n) {   // wave 0 updated row k + 1 (its first row): the next reflector
-      asm volatile("" ::: "memory");
-      tri_reflector(A, n, k + 1, vb2 + ((k + 1) & 1) * kSpdSmallMax, tau, dd, ee);
-    }
-    ADMMQ_TRI_PH(4);
-  }
-#undef ADMMQ_TRI_PH
-  if (ADMMQ_TRACE && tid == 0)
-    for (int q = 0; q < 5; ++q) g_epc_trace[8 + q] = ph[q];
-  __syncthreads();
-  if (tid == 0) {
-    if (n >= 2) {
-      dd[n - 2] = A[(n - 2) * lda + n - 2];
-      ee[n - 2] = A[(n - 2) * lda + n - 1];
-    }
-    dd[n - 1] = A[(n - 1) * lda + n - 1];
-  }
-  __syncthreads();
-}
-
-// The tridiagonalisation with the matrix in registers. Wave w holds rows r = w + 16 t (t < 9)
-// of the full symmetric matrix, lane l columns l + 64 h (h < 3): 27 doubles per lane. The
-// rank-2 update is then register-only VALU work (no LDS round trip per element: the LDS form
-// spent ~2 us per column step moving A22 through the LDS pipes), and LDS carries only the
-// vectors: v, the matvec's per-wave partial column sums (p = A v = A^T v, each wave summing
-// its own rows, the 16 partials added in wave order by one thread per column, in the free rows
-// of A past the current step), p itself. The reflector of step k + 1 is formed from registers
-// by the wave owning row k + 1, right after its update. Reflector rows go to A in LDS as
-// tri_apply_q reads them (zeros up to k, 1, v). Three workgroup barriers per step.
 constexpr int kRegRows = (kSpdSmallMax + 15) / 16;   // rows per wave (9)
 
 template <int NT>
@@ -758,9 +641,11 @@ __device__ __forceinline__ bool tri_ldl(const double* __restrict__ dd, const dou
 // thread of another wave) follows it with the derivative chains and the other four entries;
 // the row recurrences (tri_row_sums) follow B. Progress counters in LDS, advanced every
 // kTriChunk steps behind a workgroup release fence; waits are bounded (a stalled partner
-// leaves garbage, never a hang). Rows past n are zero (kTriPad), as in tri_ldl.
-__device__ __forceinline__ void tri_wait(const volatile int* prog, int need) {
-  for (int guard = 0; *prog < need && guard < (1 << 22); ++guard) __builtin_amdgcn_s_sleep(1);
+// leaves garbage and sets the stall flag, which the step reports through info; never a hang). Rows past n are zero (kTriPad), as in tri_ldl.
+__device__ __forceinline__ void tri_wait(const volatile int* prog, int need, int* stall) {
+  int guard = 0;
+  for (; *prog < need && guard < (1 << 22); ++guard) __builtin_amdgcn_s_sleep(1);
+  if (guard == (1 << 22)) *stall = 1;   // reported through info (the step's result is not trusted)
   // (a wave's LDS operations complete in order, so the loads below see what the producer
   // stored before its release; only the compiler must not hoist them above the poll)
   asm volatile("" ::: "memory");
@@ -792,10 +677,10 @@ __device__ __forceinline__ bool tri_ldl_a(const double* __restrict__ dd, const d
   return !bad;
 }
 __device__ __forceinline__ void tri_ldl_b(const double* __restrict__ ee, int n, double* __restrict__ P,
-                                          const volatile int* progA, volatile int* progB) {
+                                          const volatile int* progA, volatile int* progB, int* stall) {
   double D1 = 1.0, D2 = 0.0, L1 = 0.0, L2 = 0.0;
   for (int i = 0; i < n; ++i) {
-    if ((i & (kTriChunk - 1)) == 0) tri_wait(progA, min(i + kTriChunk, kTriPad));
+    if ((i & (kTriChunk - 1)) == 0) tri_wait(progA, min(i + kTriChunk, kTriPad), stall);
     double* Pi = P + kTriP * i;
     const double gi = Pi[3], g2 = gi * gi, e = ee[min(i, kSpdSmallMax - 1)];
     Pi[1] = L1;
@@ -808,7 +693,7 @@ __device__ __forceinline__ void tri_ldl_b(const double* __restrict__ ee, int n, 
     D2 = -e * L2;
     if ((i & (kTriChunk - 1)) == kTriChunk - 1) tri_publish(progB, i + 1);
   }
-  tri_wait(progA, kTriPad);
+  tri_wait(progA, kTriPad, stall);
   for (int i = n; i < kTriPad; ++i) {
     double* Pi = P + kTriP * i;
     Pi[1] = Pi[2] = Pi[4] = Pi[5] = 0.0;
@@ -851,12 +736,13 @@ __device__ __forceinline__ TriCoef tri_coef(const double* P, int i) {
   return TriCoef{Pi[0], Pi[1], Pi[2], Pi[3], Pi[4], Pi[5]};
 }
 __device__ __forceinline__ void tri_row_sums(const double* __restrict__ Zt, int m, int n, int row, const double* P,
-                                             const volatile int* progB, double& s0, double& s1, double& s2) {
+                                             const volatile int* progB, int* stall, double& s0, double& s1,
+                                             double& s2) {
   // every recurrence is one fma deep per step (the terms from the other chains formed off
   // it), and the sums alternate between two accumulators: a chained fp64 op costs ~30 clocks
   double u = 0.0, u1 = 0.0, u2 = 0.0;
   double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0}, a2[2] = {0.0, 0.0};
-  tri_wait(progB, min(kTriChunk, kTriPad));
+  tri_wait(progB, min(kTriChunk, kTriPad), stall);
   TriCoef cur = tri_coef(P, 0);
   auto steps = [&](const double (&zz)[kTriChunk], int i0) {   // (steps past n: P = 0, so no terms)
 #pragma unroll
@@ -886,7 +772,7 @@ __device__ __forceinline__ void tri_row_sums(const double* __restrict__ Zt, int 
   for (int i0 = 0; i0 < n; i0 += 2 * kTriChunk) {
 #pragma unroll
     for (int q = 0; q < kTriChunk; ++q) zb[q] = Zt[(size_t)min(i0 + kTriChunk + q, n - 1) * m + row];
-    tri_wait(progB, min(i0 + 2 * kTriChunk + 1, kTriPad));   // (a step reads the next step's coefficients)
+    tri_wait(progB, min(i0 + 2 * kTriChunk + 1, kTriPad), stall);   // (a step reads the next step's coefficients)
     steps(za, i0);
 #pragma unroll
     for (int q = 0; q < kTriChunk; ++q) za[q] = Zt[(size_t)min(i0 + 2 * kTriChunk + q, n - 1) * m + row];
@@ -947,10 +833,6 @@ __device__ __forceinline__ void tri_row_solve(double* __restrict__ Zt, double* _
   }
 }
 
-// mu to 1e-12 relative: X = F (G + mu I)^-1 moves by at most mu_err / (lambda_min + mu) <= 1e-12
-// relative (mu itself is ill-determined where e is flat, e'(0) = 0: there only X matters)
-constexpr double kEpcMuTol = 1e-12;
-
 __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __restrict__ G, const double* __restrict__ F,
                                                             int m, int n, double normY2, double delta2,
                                                             double* __restrict__ mu_io, double* __restrict__ X,
@@ -959,9 +841,10 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   __shared__ double dd[kSpdSmallMax], ee[kSpdSmallMax], tau[kSpdSmallMax];
   __shared__ __attribute__((aligned(16))) double cf[kTriP * kTriPad];   // the tridiagonalisation's vb (2 x n) and pb, then the LDL coefficients
   __shared__ double red[3 * kEpcThreads / 64];
-  __shared__ int s_ok;
+  __shared__ int s_ok, s_stall;
   __shared__ int s_prog[2];   // the streamed coefficients' progress (producers A, B)
-  const int tid = threadIdx.x, lda = spd_lda(n);
+  const int tid = threadIdx.x;
+  if (tid == 0) s_stall = 0;
   ADMMQ_EPC_STAMP(0);
   double tr = 0.0;   // trace(G) / n: the scale of the bracket's first step
   for (int i = tid; i < n; i += kEpcThreads) tr += G[(size_t)i * n + i];
@@ -989,57 +872,19 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
   }
   ADMMQ_EPC_STAMP(3);
   const double warm = *mu_io;
-  // The search (a state machine in LDS, thread 0 deciding between evaluations; every branch
-  // below uniform over the workgroup):
-  //   WARM   the warm start, when > 0: e < delta2 puts the root above it (mu > 0 for sure),
-  //          otherwise Newton steps go down from it inside [0, warm];
-  //   ZERO   mu = 0 (first, without a warm start; else when a Newton step from above leaves
-  //          the bracket): e(0) >= delta2 means the LS step keeps the error (mu = 0, done);
-  //   GROW   no upper end yet: from max(lo, trace / n 2^-20), doubling / Newton steps;
-  //   NEWTON safeguarded Newton inside [lo, hi] until the step is below kEpcMuTol, the bracket
-  //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
-  //          a small |e - delta2| alone does not fix mu: the step decides).
-  enum { WARM, ZERO, GROW, NEWTON, DONE };
-  struct St { double e, de, mu, lo, hi, at, pmu, q0; int state, have, need0; };   // pmu: the mu of the coefficients in LDS
-  __shared__ St st;
-  if (tid == 0) {
-    st.e = st.de = st.mu = st.lo = 0.0; st.hi = __builtin_huge_val(); st.pmu = __builtin_nan(""); st.q0 = 0.0;
-    st.state = warm > 0.0 ? WARM : ZERO; st.have = 0; st.need0 = 1;
-  }
+  // the search (epc_search.h: a state machine in LDS, thread 0 deciding between evaluations;
+  // every branch below uniform over the workgroup)
+  __shared__ EpcSearch st;
+  if (tid == 0) epc_search_init(st, warm);
   unsigned long long ev_ph[3] = {0ull, 0ull, 0ull};   // (TRACE: thread 0's LDL, row sums, block sum)
   for (int guard = 0; guard < 400; ++guard) {
     if (tid == 0) {   // where to evaluate next (or DONE)
-      for (;;) {
-        const int state = st.state;
-        if (state == WARM) { st.at = warm; break; }
-        if (state == ZERO) { st.at = 0.0; break; }
-        if (state == GROW) {
-          double at = st.have ? 2.0 * fmax(st.mu, st.lo) : (st.q0 > 0.0 ? st.q0 : (tr > 0.0 ? tr * 0x1p-20 : 1e-300));
-          if (st.have && st.de > 0.0) {   // a Newton step from below (lands above the root: e convex near it)
-            const double nx = st.mu - (st.e - delta2) / st.de;
-            if (nx > st.mu && nx < at) at = nx;
-            if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = DONE; break; }   // converged from below
-          }
-          if (!(at < 1e300)) { st.state = DONE; break; }
-          st.at = at;
-          break;
-        }
-        if (state == NEWTON) {
-          if (!(st.hi - st.lo > kEpcMuTol * st.hi)) { st.state = DONE; break; }   // collapsed bracket
-          double nx = st.de > 0.0 ? st.mu - (st.e - delta2) / st.de : -1.0;
-          if (!(nx > st.lo && nx < st.hi) && st.need0) { st.state = ZERO; continue; }   // below the bracket: is mu = 0 the answer?
-          if (!(nx > st.lo && nx < st.hi)) nx = 0.5 * (st.lo + st.hi);
-          if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = DONE; break; }   // converged
-          st.at = nx;
-          break;
-        }
-        break;   // DONE
-      }
-      if (st.state != DONE) atomicAdd(&g_epc_evals, 1ull);
+      epc_search_next(st, warm, tr, delta2);
+      if (st.state != EPC_DONE) atomicAdd(&g_epc_evals, 1ull);
     }
     if (tid == 0) { s_prog[0] = 0; s_prog[1] = 0; }
     __syncthreads();   // (also: Zt written, before the first evaluation)
-    if (st.state == DONE) break;
+    if (st.state == EPC_DONE) break;
     const double at = st.at;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     const unsigned long long t1 = ADMMQ_NOW();
@@ -1048,56 +893,17 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
     if (tid == 64) {
       s_ok = tri_ldl_a(dd, ee, n, at, cf, &s_prog[0]) ? 1 : 0;
     } else if (tid == 128) {
-      tri_ldl_b(ee, n, cf, &s_prog[0], &s_prog[1]);
+      tri_ldl_b(ee, n, cf, &s_prog[0], &s_prog[1], &s_stall);
     } else if (tid < 64 || tid >= 192) {
       for (int row = tid < 64 ? tid : tid - 128; row < m; row += kEpcThreads - 128)
-        tri_row_sums(Zt, m, n, row, cf, &s_prog[1], s0, s1, s2);
+        tri_row_sums(Zt, m, n, row, cf, &s_prog[1], &s_stall, s0, s1, s2);
     }
     const unsigned long long t2 = ADMMQ_NOW();
     block_sum3<kEpcThreads>(s0, s1, s2, red);
     ev_ph[1] += t2 - t1;
     ev_ph[2] += ADMMQ_NOW() - t2;
-    if (tid == 0) {
-      // e = ||Y||^2 - <F, X> - mu ||X||^2 with <F, X> = s, ||X||^2 = -s'; e' = mu s''
-      const bool ok = s_ok != 0;
-      st.pmu = ok ? at : __builtin_nan("");
-      const double en = normY2 - s0 + at * s1, dn = at * s2;
-      const int state = st.state;
-      if (state == WARM) {
-        // above the root: Newton down from the warm start, e(0) only if a step leaves the
-        // bracket (the LS step may keep the error: mu = 0); below it: grow
-        if (ok) {
-          st.mu = at; st.e = en; st.de = dn; st.have = 1;
-          if (en < delta2) { st.lo = at; st.need0 = 0; }
-          else st.hi = at;
-        }
-        st.state = !ok ? ZERO : (st.need0 ? NEWTON : GROW);
-      } else if (state == ZERO) {
-        if (ok && en >= delta2) { st.mu = 0.0; st.have = 0; st.state = DONE; }   // the LS step: mu = 0
-        else {
-          // a cold start's first step from the model e(mu) ~ e(0) + mu^2 <X0, X0 G^-1> near 0
-          // (e' = 2 mu <X, X A^-1>, and s'' / 2 = <X, X A^-1>): it lands at or below the root
-          // where <X, X A^-1> falls with mu, so the growth continues from there
-          if (ok && s2 > 0.0) st.q0 = sqrt((delta2 - en) / (0.5 * s2));
-          st.need0 = 0;
-          st.state = (st.have && st.hi < __builtin_huge_val()) ? NEWTON : GROW;
-        }
-      } else if (state == GROW) {
-        if (!ok) st.lo = at;
-        else {
-          st.mu = at; st.e = en; st.de = dn; st.have = 1;
-          if (en < delta2) st.lo = at;
-          else { st.hi = at; st.state = NEWTON; }
-        }
-      } else if (state == NEWTON) {
-        if (!ok) st.lo = at;
-        else {
-          st.mu = at; st.e = en; st.de = dn;
-          if (en < delta2) { st.lo = at; st.need0 = 0; } else st.hi = at;   // (e increases with mu: e(0) <= e(lo))
-          if (fabs(en - delta2) <= 16.0 * 0x1p-52 * normY2) st.state = DONE;   // at the rounding floor of e
-        }
-      }
-    }
+    if (tid == 0)   // e = ||Y||^2 - <F, X> - mu ||X||^2 with <F, X> = s, ||X||^2 = -s'; e' = mu s''
+      epc_search_absorb(st, s_ok != 0, normY2 - s0 + at * s1, at * s2, 0.5 * s2, delta2, normY2);
   }
   ADMMQ_EPC_STAMP(4);
   if (ADMMQ_TRACE && tid == 0)
@@ -1127,7 +933,12 @@ __global__ __launch_bounds__(kEpcThreads) void k_epc_step64(const double* __rest
         if (j < n) X[(size_t)row * n + j] = ok ? y[q] : __builtin_nan("");
       }
   }
-  if (tid == 0) { *mu_io = st.mu; if (info) *info = ok && (st.have || st.mu == 0.0) ? 0 : 1; }
+  // info 1: no positive definite G + mu I on the bracket, the search's evaluation budget
+  // spent, or a stalled coefficient hand-off (a bounded wait expired: its sums are not trusted)
+  if (tid == 0) {
+    *mu_io = st.mu;
+    if (info) *info = ok && st.state == EPC_DONE && !s_stall && (st.have || st.mu == 0.0) ? 0 : 1;
+  }
   ADMMQ_EPC_STAMP(5);
 }
 
@@ -1150,6 +961,15 @@ __global__ __launch_bounds__(256) void k_cp_colnorm(CpColNorm a, int R) {
   const double nrm = fmax(sqrt(acc), 1e-300);
 #pragma unroll 8
   for (int i = 0; i < I; ++i) dst[(size_t)i * R + r] = src[(size_t)i * R + r] / nrm;
+}
+
+void launch_spd_solve64_small(const double* G, const double* F, int m, int n, double rel_shift, double* X, int* info,
+                              hipStream_t s) {
+  const size_t lds = (size_t)n * spd_lda(n) * sizeof(double);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_spd_solve64), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL(k_spd_solve64, dim3(1), dim3(kSpdThreads), lds, s, G, F, m, n, rel_shift, X, info);
 }
 
 }  // namespace admmq
@@ -1199,12 +1019,7 @@ int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n
   if (!G || !F || !X || m < 0 || n <= 0 || n > kSpdSmallMax || m > (1LL << 24))
     return set_error(ADMMQ_ERR_ARG, "spd_solve64: bad arguments (1 <= n <= 136)");
   if (m == 0) return ADMMQ_OK;
-  const size_t lds = (size_t)n * spd_lda((int)n) * sizeof(double);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_spd_solve64), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL(k_spd_solve64, dim3(1), dim3(kSpdThreads), lds, static_cast<hipStream_t>(stream), G, F, (int)m,
-                     (int)n, X, info);
+  launch_spd_solve64_small(G, F, (int)m, (int)n, 0.0, X, info, static_cast<hipStream_t>(stream));
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : set_error(ADMMQ_ERR_HIP, "spd_solve64: launch failed");
 }
 

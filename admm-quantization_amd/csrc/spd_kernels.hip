@@ -355,7 +355,11 @@ __global__ __launch_bounds__(256) void k_minv(const ProbDesc* __restrict__ probs
   }
 }
 
-void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s) {
+// L (lower, in A64) and Linv = L^-1 (lower blocks of L64; the upper off-diagonal blocks are
+// not written) of A64 = L L^T; flags[2] on a non-positive pivot. Every launch reads the block
+// count from the descriptor, so a descriptor whose nbk is 0 turns them all into no-ops (the
+// blocked EPC step's rounds after its search is done, solve64.hip).
+void launch_spd_linv(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s) {
   for (int k = 0; k < maxnbk; ++k) {
     hipLaunchKernelGGL(k_chol_panel, dim3(maxnbk - k, nprob), dim3(256), 0, s, d, k);
     const int n = maxnbk - k - 1;
@@ -369,6 +373,10 @@ void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s)
   } else {   // panel would not fit in LDS: one launch per block row
     for (int i = 0; i < maxnbk; ++i) hipLaunchKernelGGL(k_linv_row, dim3(i + 1, nprob), dim3(256), 0, s, d, i);
   }
+}
+
+void launch_spd_inverse(const ProbDesc* d, int nprob, int maxnbk, hipStream_t s) {
+  launch_spd_linv(d, nprob, maxnbk, s);
   hipLaunchKernelGGL(k_minv, dim3(maxnbk * (maxnbk + 1) / 2, nprob), dim3(256), 0, s, d);
 }
 

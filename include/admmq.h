@@ -29,6 +29,11 @@
  *                                           rho,max_iter,eps): the updates around the projection, device break test
  *   admmq_panel_xtq / _xy / _outer       <- scripts/factorize_lowrank.py:80-82 (torch.linalg.svd + the rank-r
  *                                           product): the X^T Q, X Y and U S V^T products of the device projection
+ *   admmq_cp64_gram_mttkrp               <- source/parafac_epc.py:42-74 (tensorly parafac / musco cp_anc's MTTKRP and
+ *                                           Gram-Hadamard products, fp64)
+ *   admmq_spd_solve64(_ws)               <- source/parafac_epc.py:42 (parafac's torch.linalg.solve(G, F.T).T)
+ *   admmq_epc_step64 / admmq_epc_*64     <- source/parafac_epc.py:61-74 (cp_anc's mode update: eigendecomposition
+ *                                           of G and the multiplier of the error constraint)
  */
 #ifndef ADMMQ_H_
 #define ADMMQ_H_
@@ -293,20 +298,56 @@ int32_t admmq_epc_mu(const double* c, const double* s, int64_t n, double normY2,
 /* The R x R solves of the CP-ALS / EPC initialiser on one workgroup (the fp64 matrix in LDS,
  * 1 <= n <= 136), replacing tensorly parafac's torch.linalg.solve and cp_anc's eigendecomposition
  * (source/parafac_epc.py:42, :61-74). Row-major device doubles; no host synchronisation.
- *   admmq_spd_solve64  X = F G^-1 (F, X: m x n; G: n x n SPD); *info (device int, may be NULL)
- *                      = 0, or 1 when G is not positive definite (X untouched).
+ *   admmq_spd_solve64  X = F G^-1 (F, X: m x n; G: n x n SPD) by an unpivoted blocked Gauss-Jordan
+ *                      inverse of G in LDS; *info (device int, may be NULL) = 0, or 1 when a pivot
+ *                      is not positive (G not numerically positive definite: X untouched).
  *   admmq_epc_step64   X = F (G + mu I)^-1 with mu >= 0 the root of
  *                      normY2 - <F, X> - mu ||X||^2 = delta2 (= the eigen form
  *                      normY2 - sum_j |F v_j|^2 (s_j + 2 mu) / (s_j + mu)^2), 0 when the LS step's
  *                      error already reaches delta2; *mu (device double): in, a warm start (<= 0:
  *                      none), out, the root. work: m x n device doubles of scratch (F Q and the
  *                      solved rows, transposed: G = Q T Q^T is tridiagonalised once per call).
+ *                      G is reduced to tridiagonal form once (Householder), every evaluation of
+ *                      the error equation is then a set of tridiagonal L D L^T recurrences.
  *                      *info (may be NULL): 0, or 1 when no G + mu I on the search bracket was
- *                      positive definite (X NaN). */
+ *                      positive definite (X NaN), the search's budget ran out or an internal
+ *                      hand-off timed out. */
 int32_t admmq_spd_solve64(const double* G, const double* F, int64_t m, int64_t n, double* X, int32_t* info,
                           void* stream);
 int32_t admmq_epc_step64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
                          double* mu, double* X, double* work, int32_t* info, void* stream);
+
+/* The same solves for any n (1 <= n <= 8192), spread over the chip (the resnet ranks 183 ... 1141 do
+ * not fit one workgroup's LDS): A = G + shift I (fp64, shift = rel_shift * trace(G) / n), its
+ * blocked Cholesky A = L L^T and L^-1 (the 32 x 32-blocked fp64 kernels of the ADMM prepare),
+ * then X = (F L^-T) L^-1 as two fp64-MFMA GEMMs. Caller-owned workspace of
+ * admmq_solve64_workspace_size(m, n) bytes (no initialisation; calls on one workspace must be
+ * stream-ordered); no host synchronisation.
+ *   admmq_spd_solve64_ws   X = F (G + shift I)^-1 (replaces source/parafac_epc.py:42, tensorly parafac's
+ *                          torch.linalg.solve(G, F.T).T); *info (device int, may be NULL) = 0, or 1
+ *                          when G + shift I is not numerically positive definite (X undefined). n <= 136
+ *                          runs the one-workgroup kernel of admmq_spd_solve64 (no workspace used).
+ *   admmq_epc_begin64 / admmq_epc_rounds64 / admmq_epc_end64
+ *                          the EPC mode update of admmq_epc_step64 (replaces source/parafac_epc.py:61-74,
+ *                          musco cp_anc's eigendecomposition) for any n: begin sets the multiplier
+ *                          search up on the device (*mu: the warm start, <= 0 none); each round is one
+ *                          evaluation (a Cholesky of G + mu I at the search's next mu, X = F (G + mu I)^-1,
+ *                          and the Newton update of mu on the device); rounds after the search is done
+ *                          return at once. *done (device int, may be NULL) = 1 once it is done: the
+ *                          caller reads it when it chooses and asks for more rounds until then.
+ *                          end writes *mu (device double) and *info (device int, may be NULL): 0
+ *                          converged (X = F (G + mu I)^-1 at the returned mu), 1 no positive definite
+ *                          G + mu I found or the evaluation budget (96) spent, 2 not done yet. The same
+ *                          G, F, X, m, n and workspace for every call of one step. */
+size_t admmq_solve64_workspace_size(int64_t m, int64_t n);
+int32_t admmq_spd_solve64_ws(const double* G, const double* F, int64_t m, int64_t n, double rel_shift, double* X,
+                             int32_t* info, void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_epc_begin64(const double* G, const double* F, int64_t m, int64_t n, double normY2, double delta2,
+                          const double* mu, double* X, void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_epc_rounds64(const double* G, const double* F, int64_t m, int64_t n, double* X, int32_t rounds,
+                           int32_t* done, void* workspace, size_t workspace_bytes, void* stream);
+int32_t admmq_epc_end64(int64_t m, int64_t n, double* mu, int32_t* info, void* workspace, size_t workspace_bytes,
+                        void* stream);
 
 /* cp_anc's normalisation of the factors other than the one being updated
  * (source/parafac_epc.py:61-74, musco cp_anc): outA = A / max(||A[:, r]||_2, 1e-300) per column r

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """F11: the reference's own spread at the benchmarked horizon (survey container only).
 
-Run:  python3 -B tests/golden/gen_f11_horizon.py [--reference /root/reference] [--trials 5]
+Run:  python3 -B tests/golden/gen_f11_horizon.py [--reference /root/reference] [--trials 5] [--threads 1,2,4,8]
 
 bench.py times max_iter_admm = 1000 (999 inner iterations, eps = 0; scripts/factorize.py:
 218-221). At that horizon the reference is chaotic at the 1-ulp level: two
@@ -16,7 +16,11 @@ oracle's Gram / MTTKRP - the inputs tests/test_gpu_horizon.py feeds the device):
     proxy; no reference file is touched): the objective ||F - H G|| / ||F|| (float64)
     and the 4-bit grid step of every run;
   * one ALS sweep (the three modes in sequence, scripts/factorize.py:207-266) the same
-    way: the sweep's rec_error and quant_rec_error.
+    way: the sweep's rec_error and quant_rec_error;
+  * all of it at every torch CPU thread count of ``--threads`` (F4's method): the
+    reference's matmul / cholesky_solve summation order follows the thread count, a spread
+    the 1-ulp proxy alone does not explore. ``runs`` records each run's thread count and
+    trial (0 = unperturbed).
 
 Writes data only: tests/golden/f11_horizon.json.
 """
@@ -68,12 +72,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--trials", type=int, default=5)
+    ap.add_argument("--threads", default="1,2,4,8")
     a = ap.parse_args()
-    torch.set_num_threads(8)
+    threads = [int(t) for t in a.threads.split(",")]
     ref_admm, ref_quant = import_reference(a.reference)
     W, R, fs0 = c2_start()
     out = {"config": "C2 resnet18 layer1.0.conv1 R=134, seed-42 random start, U=0, 4-bit mse-minmax, eps=0",
-           "max_iter_admm": MAX_ITER, "trials_perturbed": a.trials, "torch": torch.__version__, "threads": 8,
+           "max_iter_admm": MAX_ITER, "trials_perturbed": a.trials, "torch": torch.__version__, "threads": threads,
+           "runs": [[nt, t] for nt in threads for t in range(a.trials + 1)],
            "modes": {}, "sweep": {"rec_error": [], "quant_rec_error": []}}
 
     def run(H0, F, G, rng):
@@ -88,16 +94,18 @@ def main():
     for mode in range(3):
         G, F = ao.gram_mttkrp(W, fs0, mode)
         objs, steps = [], []
-        for t in range(a.trials + 1):
+        for nt, t in out["runs"]:
+            torch.set_num_threads(nt)
             t0 = time.time()
-            h = run(fs0[mode], F, G, None if t == 0 else np.random.default_rng(5000 + 10 * mode + t))
+            h = run(fs0[mode], F, G, None if t == 0 else np.random.default_rng(5000 + 10 * mode + t + 1000 * nt))
             objs.append(objective(F, G, h))
             steps.append(grid_step(h))
-            print(f"mode {mode} trial {t}: objective {objs[-1]:.6e} step {steps[-1]:.4e} ({time.time() - t0:.1f} s)",
-                  flush=True)
+            print(f"mode {mode} threads {nt} trial {t}: objective {objs[-1]:.6e} step {steps[-1]:.4e} "
+                  f"({time.time() - t0:.1f} s)", flush=True)
         out["modes"][str(mode)] = {"objective": objs, "grid_step": steps}
-    for t in range(a.trials + 1):
-        rng = None if t == 0 else np.random.default_rng(7000 + t)
+    for nt, t in out["runs"]:
+        torch.set_num_threads(nt)
+        rng = None if t == 0 else np.random.default_rng(7000 + t + 1000 * nt)
         fs = [f.copy() for f in fs0]
         qf = [None] * 3
         for m in range(3):
@@ -110,7 +118,7 @@ def main():
         out["sweep"]["rec_error"].append(float(ref_admm.squared_relative_diff(Wt, torch.einsum("ir,jr,kr->ijk", *rec))))
         out["sweep"]["quant_rec_error"].append(
             float(ref_admm.squared_relative_diff(Wt, torch.einsum("ir,jr,kr->ijk", *recq))))
-        print(f"sweep trial {t}: rec {out['sweep']['rec_error'][-1]:.6f} quant {out['sweep']['quant_rec_error'][-1]:.6f}",
+        print(f"sweep threads {nt} trial {t}: rec {out['sweep']['rec_error'][-1]:.6f} quant {out['sweep']['quant_rec_error'][-1]:.6f}",
               flush=True)
     with open(os.path.join(HERE, "f11_horizon.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -189,8 +189,32 @@ def test_epc_solves_refuse_bad_arguments(lib):
         panel.colnorm64(F)                                                 # a CPU tensor
     with pytest.raises(ValueError):
         panel.spd_solve64(G.float(), F)                                    # float32
-    with pytest.raises(ValueError):
+    with pytest.raises(RuntimeError, match="ROCm GPU"):                  # a CPU tensor (n > 136: the blocked step)
         panel.epc_step64(torch.eye(137, dtype=torch.float64), torch.randn(2, 137, dtype=torch.float64), 1.0, 0.5,
                          torch.zeros((), dtype=torch.float64))
     with pytest.raises(RuntimeError, match="ROCm GPU"):
+        panel.spd_solve64(torch.eye(200, dtype=torch.float64), torch.randn(2, 200, dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
         parafac_epc(torch.randn(4, 5, 6, dtype=torch.float64), 3)
+
+
+def test_blocked_solves_check_arguments(lib):
+    """The blocked R x R solves (csrc/solve64.hip: any n) size their workspace from (m, n) alone
+    and refuse bad arguments or a short workspace on the host, before any launch."""
+    p = ctypes.c_void_p(0x1000)
+    ERR_ARG, ERR_WS = -1, -3
+    assert lib.admmq_solve64_workspace_size(0, 5) == 0
+    assert lib.admmq_solve64_workspace_size(4, 0) == 0
+    big = lib.admmq_solve64_workspace_size(512, 1141)
+    assert big >= 2 * 1152 * 1152 * 8 + 2 * 512 * 1141 * 8                # A, L^-1 and the two m x n products
+    assert big == lib.admmq_solve64_workspace_size(512, 1141)               # a function of (m, n) only
+    assert lib.admmq_solve64_workspace_size(9, 1141) < big
+    assert lib.admmq_spd_solve64_ws(None, p, 4, 200, 0.0, p, None, p, 1 << 30, None) == ERR_ARG
+    assert lib.admmq_spd_solve64_ws(p, p, 4, 200, -1.0, p, None, p, 1 << 30, None) == ERR_ARG   # negative shift
+    assert lib.admmq_spd_solve64_ws(p, p, 4, 200, 0.0, p, None, p, 8, None) == ERR_WS
+    assert lib.admmq_epc_begin64(p, p, 4, 200, 1.0, 0.5, None, p, p, 1 << 30, None) == ERR_ARG   # no mu
+    assert lib.admmq_epc_begin64(p, p, 4, 200, 1.0, 0.5, p, p, p, 8, None) == ERR_WS
+    assert lib.admmq_epc_rounds64(p, p, 4, 200, p, -1, None, p, 1 << 30, None) == ERR_ARG
+    assert lib.admmq_epc_rounds64(p, p, 4, 200, p, 1, None, p, 8, None) == ERR_WS
+    assert lib.admmq_epc_end64(0, 200, p, None, p, 1 << 30, None) == ERR_ARG
+    assert lib.admmq_epc_end64(4, 200, p, None, p, 8, None) == ERR_WS

@@ -119,7 +119,7 @@ def test_epc_mu_device_matches_oracle(R, seed):
 
 @pytest.mark.parametrize("n,m", [(1, 3), (5, 9), (64, 1), (134, 64), (134, 9), (136, 130)])
 def test_spd_solve64_vs_library(n, m):
-    """The one-workgroup fp64 solve (csrc/epc_kernels.hip: Cholesky with the matrix in LDS,
+    """The one-workgroup fp64 solve (csrc/epc_kernels.hip: Gauss-Jordan inverse in LDS,
     16-lane substitution groups) that replaces tensorly parafac's torch.linalg.solve
     (source/parafac_epc.py:42): X = F G^-1 within 1e-11 of the float64 library solve on a
     well-conditioned SPD G, at n up to the LDS limit and m above one pass of 64 rows."""

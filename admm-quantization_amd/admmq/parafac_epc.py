@@ -100,6 +100,15 @@ def _drive(gen):
         return stop.value
 
 
+def _colnorms(U: torch.Tensor) -> torch.Tensor:
+    """Column 2-norms (the ||U[:, r]|| of tensorly / musco's normalisations)."""
+    return torch.sqrt(torch.sum(U * U, dim=0))
+
+
+def _norm(v: torch.Tensor) -> torch.Tensor:
+    return torch.sqrt(torch.sum(v * v))
+
+
 def _cp_error2(normY2, F_last: torch.Tensor, G_last: torch.Tensor, U_last: torch.Tensor,
                weights: Optional[torch.Tensor] = None) -> torch.Tensor:
     """||Y - [[w; U]]||^2 (a 0-dim device tensor: no host synchronisation) from the last
@@ -157,7 +166,7 @@ def _parafac_gen(tensor, rank: int, init: str = "random", random_state=None, tol
     weights = torch.ones(rank, dtype=torch.float64, device=X.device)
     if normalize_factors:
         for m in range(n):
-            nrm = torch.linalg.norm(fs[m], dim=0)
+            nrm = _colnorms(fs[m])
             weights = weights * nrm
             fs[m] = fs[m] / nrm
     return weights, fs
@@ -169,7 +178,8 @@ def parafac(tensor: torch.Tensor, rank: int, init: str = "random", random_state=
     return _drive(_parafac_gen(tensor, rank, init, random_state, tol, n_iter_max, normalize_factors))
 
 
-def _cp_anc_gen(tensor, rank: int, delta: float, weights=None, factors=None, maxiter: int = 5000, tol: float = 1e-5):
+def _cp_anc_gen(tensor, rank: int, delta: float, weights=None, factors=None, maxiter: int = 5000, tol: float = 1e-5,
+                mus=None):
     Y = _on_gpu64(tensor).contiguous()
     n = Y.dim()
     fs = [f.to(device=Y.device, dtype=torch.float64).clone() for f in factors]
@@ -178,7 +188,8 @@ def _cp_anc_gen(tensor, rank: int, delta: float, weights=None, factors=None, max
     (ny,) = yield from _host(torch.sum(Y * Y))
     normY2 = float(ny)
     delta2 = float(delta) ** 2
-    mus = [torch.zeros((), dtype=torch.float64, device=Y.device) for _ in range(n)]   # warm starts per mode
+    if mus is None:   # the multipliers' warm starts per mode (parafac_epc carries them across its rounds)
+        mus = [torch.zeros((), dtype=torch.float64, device=Y.device) for _ in range(n)]
     lam_prev = None
     it, total = 0, max(int(maxiter), 1)
     while it < total:
@@ -201,7 +212,7 @@ def _cp_anc_gen(tensor, rank: int, delta: float, weights=None, factors=None, max
                     fs[m] = epc_step64(G, F, normY2, delta2, mus[m], info=info)
                 else:
                     fs[m] = yield from epc_step64_gen(G, F, normY2, delta2, mus[m], info=info)
-            lnorms.append(torch.linalg.norm(torch.linalg.norm(fs[n - 1], dim=0)))
+            lnorms.append(_norm(_colnorms(fs[n - 1])))
             snaps.append(list(fs))
         it += steps
         lv, iv = yield from _host(torch.stack(lnorms), infos)   # the chunk's one host read
@@ -220,7 +231,7 @@ def _cp_anc_gen(tensor, rank: int, delta: float, weights=None, factors=None, max
     # final normalisation: every factor unit-norm columns, intensities in the weights
     weights = torch.ones(rank, dtype=torch.float64, device=Y.device)
     for m in range(n):
-        nrm = torch.linalg.norm(fs[m], dim=0).clamp_min(1e-300)
+        nrm = _colnorms(fs[m]).clamp_min(1e-300)
         weights = weights * nrm
         fs[m] = fs[m] / nrm
     return weights, fs
@@ -244,14 +255,15 @@ def _parafac_epc_gen(tensor, rank, als_maxiter=5000, als_tol=1e-5, num_threads=4
     last = Y.dim() - 1
     F, G = gram_mttkrp_f64(Y, fs, last)
     d2, ln, lmax, lmin = yield from _host(_cp_error2(torch.sum(Y * Y), F, G, fs[last], lmbda),
-                                          torch.linalg.norm(lmbda), lmbda.max(), lmbda.min())
+                                          _norm(lmbda), lmbda.max(), lmbda.min())
     delta = float(d2) ** 0.5
     lambda_norm_prev = float(ln)
     alpha_prev = float(lmax) / float(lmin)
     stopflag = 0
+    mus = [torch.zeros((), dtype=torch.float64, device=Y.device) for _ in range(Y.dim())]
     for _ in range(epc_rounds):
-        lmbda, fs = yield from _cp_anc_gen(Y, rank, delta, lmbda, fs, maxiter=epc_maxiter, tol=epc_tol)
-        ln, lmax, lmin = yield from _host(torch.linalg.norm(lmbda), lmbda.max(), lmbda.min())
+        lmbda, fs = yield from _cp_anc_gen(Y, rank, delta, lmbda, fs, maxiter=epc_maxiter, tol=epc_tol, mus=mus)
+        ln, lmax, lmin = yield from _host(_norm(lmbda), lmbda.max(), lmbda.min())
         lambda_norm = float(ln)
         alpha = float(lmax) / float(lmin)
         if abs(lambda_norm_prev - lambda_norm) < stop_tol * lambda_norm_prev:

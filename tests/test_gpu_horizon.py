@@ -4,17 +4,17 @@ bench.py times. Shorter-horizon parity (one step bit-level, 30 steps at the larg
 the 20 x 20 ALS band) is in test_gpu_parity.py; here the contract is what survives 999
 chaotic iterations. The reference is not reproducible against itself at this horizon
 (SURVEY.md §0, F8): F11 (tests/golden/gen_f11_horizon.py) re-ran the reference's own
-admm_iteration on C2 from the same start with its cholesky_solve moved by <= 1 ulp, and
-its objective ||F - H G|| / ||F|| spreads over ~2 % (mode 0: 0.1582 ... 0.1610), so the
-contract is that band (widened by half its width, the F10 rule), not a 1e-3 match to any
-one run:
+admm_iteration on C2 from the same start at torch CPU thread counts {1, 2, 4, 8} (F4's
+method: the thread count moves the summation order) and, at each, with its cholesky_solve
+moved by <= 1 ulp (F8's proxy) - 24 runs - and its objective ||F - H G|| / ||F|| spreads over
+~2 % (mode 0: 0.1581 ... 0.1610), so the contract is that band (widened by half its width,
+the F10 rule), not a 1e-3 match to any one run:
 
   * C2 (resnet18 layer1.0.conv1, every mode from the same seed-42 start, F and G from the
     oracle): the reference's iteration count, every result on a 4-bit grid (<= 16 levels),
-    and the 999-iteration result's objective and grid step inside the reference's F11 band
-    (the step's band widened by one MSE candidate's spacing) or, where the CPU oracle's run
-    of the same call lands outside it too (mode 2: F11's 1-ulp perturbations explore less
-    than another summation order does), no farther outside than the oracle;
+    and the 999-iteration result's objective and grid step inside the reference's F11 band;
+    the CPU oracle's run of the same call (an independent float32 restatement) inside it
+    too (mode 2: the reference's one-thread runs reach 0.11946, where the oracle lands);
   * C2 as one ALS sweep (the three modes in sequence, the reference loop): the sweep's
     reconstruction errors (rec_error, quant_rec_error) inside the reference's F11 sweep band;
   * C3 (all 16 resnet18 3x3 convs batched, the bench's step): property checks on every
@@ -42,11 +42,6 @@ def _band(vals):
     lo, hi = min(vals), max(vals)
     w = 0.5 * (hi - lo)
     return lo - w, hi + w
-
-
-def _outside(v, lo, hi):
-    """Distance of v outside [lo, hi] (0 inside)."""
-    return max(lo - v, v - hi, 0.0)
 
 
 @pytest.fixture(scope="module")
@@ -105,16 +100,11 @@ def test_c2_mode_call_at_bench_horizon(torch_dev, mode):
     print(f"C2 mode {mode}, {MAX_ITER - 1} its: objective gpu {og:.6e}, oracle {oo:.6e}, "
           f"reference runs {min(ref['objective']):.6e} .. {max(ref['objective']):.6e}; grid step gpu {sg:.4e}, "
           f"oracle {so:.4e}, reference {min(ref['grid_step']):.4e} .. {max(ref['grid_step']):.4e}")
-    # inside the band, or no farther outside it than the CPU restatement of the same call: F11's
-    # 1-ulp proxy explores less than a different summation order does (mode 2: the oracle lands
-    # 0.7 % above the band, the device 0.06 %). The grid step is one of the MSE search's 200
-    # candidates (t_c = mx (0.2 + c / 199), quantization.py:129-144): a run on another branch
-    # picks a neighbouring candidate, so its band is widened by one candidate's spacing at the
-    # top of the grid, the smallest relative spacing there is (1 / 238.8)
-    assert _outside(og, lo, hi) <= _outside(oo, lo, hi), (og, oo, lo, hi)
-    cand = 1.0 / (0.2 * 199 + 199)
-    slo, shi = slo * (1 - cand), shi * (1 + cand)
-    assert _outside(sg, slo, shi) <= _outside(so, slo, shi), (sg, so, slo, shi)
+    meta = json.load(open(F11))
+    assert meta["threads"] == [1, 2, 4, 8] and len(ref["objective"]) == len(meta["runs"]) == 24
+    assert lo <= og <= hi, (og, lo, hi)
+    assert slo <= sg <= shi, (sg, slo, shi)
+    assert lo <= oo <= hi and slo <= so <= shi, (oo, so, lo, hi, slo, shi)   # the oracle is inside too
 
 
 def test_c2_sweep_at_bench_horizon(torch_dev):

@@ -299,9 +299,11 @@ void cp64_plan_gemm(Cp64Plan& pl, const double* A, long long lda, const double* 
   f.X = B; f.ldb = ldb; f.bt = bt; f.tri = tri;
   f.out = C; f.gate = gate;
   const int tm = cdiv64(M, kC64BM), tn = cdiv64(N, kC64BN);
-  // K chunks of >= 64 to bring the units to ~512 (2 per CU): a 64 x 64 tile's K chain is
-  // latency-bound at these sizes (k_cp64's staging waits on each step's loads)
-  const int by_k = std::max(1, K / 64), by_fill = std::max(1, 512 / std::max(tm * tn, 1));
+  // K chunks of >= 64 to bring the units to ~2048 (8 per CU): a 64 x 64 tile's K chain is
+  // latency-bound at these sizes (each K-step of k_cp64 waits on its staging loads), so short
+  // chains side by side beat long ones; the fixed-order reduction reads the extra planes once
+  // (with a triangular B most chunks of the early column tiles are empty and return at once)
+  const int by_k = std::max(1, K / 64), by_fill = std::max(1, 2048 / std::max(tm * tn, 1));
   f.nsplit = std::max(1, std::min(by_k, by_fill));
   f.kchunk = cdiv64(cdiv64(K, f.nsplit), kC64BK) * kC64BK;
   f.nsplit = cdiv64(K, f.kchunk);

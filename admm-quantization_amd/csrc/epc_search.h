@@ -14,7 +14,10 @@
 //   GROW   no upper end yet: from max(lo, trace / n 2^-20), doubling / Newton steps;
 //   NEWTON safeguarded Newton inside [lo, hi] until the step is below kEpcMuTol, the bracket
 //          has collapsed or e is at its rounding floor (e is flat near mu = 0, e'(0) = 0, so
-//          a small |e - delta2| alone does not fix mu: the step decides).
+//          a small |e - delta2| alone does not fix mu: the step decides). A point reached by
+//          a Newton step of relative size <= kEpcMuQuad is accepted without evaluating the
+//          next step: Newton converges quadratically, so that step would be ~kEpcMuQuad^2
+//          (the confirming evaluation was a third of a warm-started step's evaluations).
 // A failed factorisation at mu (G + mu I not numerically positive definite) only raises lo.
 #pragma once
 
@@ -23,11 +26,13 @@ namespace admmq {
 // mu to 1e-12 relative: X = F (G + mu I)^-1 moves by at most mu_err / (lambda_min + mu) <= 1e-12
 // relative (mu itself is ill-determined where e is flat, e'(0) = 0: there only X matters)
 constexpr double kEpcMuTol = 1e-12;
+constexpr double kEpcMuQuad = 1e-6;   // sqrt(kEpcMuTol)
 
 enum { EPC_WARM = 0, EPC_ZERO, EPC_GROW, EPC_NEWTON, EPC_DONE, EPC_FINAL };
 
 // pmu: the mu of the last successful evaluation (NaN after a failed one)
-struct EpcSearch { double e, de, mu, lo, hi, at, pmu, q0; int state, have, need0, pad_; };
+// lastrel: the relative size of the Newton step that chose `at` (infinite for other choices)
+struct EpcSearch { double e, de, mu, lo, hi, at, pmu, q0, lastrel; int state, have, need0, pad_; };
 
 __host__ __device__ inline void epc_search_init(EpcSearch& st, double warm) {
   st.e = st.de = st.mu = st.lo = 0.0;
@@ -35,6 +40,7 @@ __host__ __device__ inline void epc_search_init(EpcSearch& st, double warm) {
   st.pmu = __builtin_nan("");
   st.q0 = 0.0;
   st.at = 0.0;
+  st.lastrel = __builtin_huge_val();
   st.state = warm > 0.0 ? EPC_WARM : EPC_ZERO;
   st.have = 0;
   st.need0 = 1;
@@ -47,6 +53,10 @@ __host__ __device__ inline void epc_search_next(EpcSearch& st, double warm, doub
     const int state = st.state;
     if (state == EPC_WARM) { st.at = warm; return; }
     if (state == EPC_ZERO) { st.at = 0.0; return; }
+    // the point just evaluated came from a Newton step of relative size <= kEpcMuQuad (and
+    // was factorised): accept it
+    if (st.lastrel <= kEpcMuQuad && st.pmu == st.mu && st.pmu == st.at) { st.state = EPC_DONE; return; }
+    st.lastrel = __builtin_huge_val();
     if (state == EPC_GROW) {
       double at = st.have ? 2.0 * fmax(st.mu, st.lo) : (st.q0 > 0.0 ? st.q0 : (tr > 0.0 ? tr * 0x1p-20 : 1e-300));
       // no successful evaluation yet but failed ones: a shift too small to factor, so the next
@@ -54,8 +64,8 @@ __host__ __device__ inline void epc_search_next(EpcSearch& st, double warm, doub
       if (!st.have && st.lo > 0.0) at = fmax(at, 2.0 * st.lo);
       if (st.have && st.de > 0.0) {   // a Newton step from below (lands above the root: e convex near it)
         const double nx = st.mu - (st.e - delta2) / st.de;
-        if (nx > st.mu && nx < at) at = nx;
         if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = EPC_DONE; return; }   // converged from below
+        if (nx > st.mu && nx < at) { at = nx; st.lastrel = (nx - st.mu) / st.mu; }
       }
       if (!(at < 1e300)) { st.state = EPC_DONE; return; }
       st.at = at;
@@ -65,8 +75,10 @@ __host__ __device__ inline void epc_search_next(EpcSearch& st, double warm, doub
       if (!(st.hi - st.lo > kEpcMuTol * st.hi)) { st.state = EPC_DONE; return; }   // collapsed bracket
       double nx = st.de > 0.0 ? st.mu - (st.e - delta2) / st.de : -1.0;
       if (!(nx > st.lo && nx < st.hi) && st.need0) { st.state = EPC_ZERO; continue; }   // below the bracket: is mu = 0 the answer?
-      if (!(nx > st.lo && nx < st.hi)) nx = 0.5 * (st.lo + st.hi);
+      const bool newton = nx > st.lo && nx < st.hi;
+      if (!newton) nx = 0.5 * (st.lo + st.hi);
       if (fabs(nx - st.mu) <= kEpcMuTol * st.mu) { st.state = EPC_DONE; return; }   // converged
+      if (newton && st.mu > 0.0) st.lastrel = fabs(nx - st.mu) / st.mu;
       st.at = nx;
       return;
     }

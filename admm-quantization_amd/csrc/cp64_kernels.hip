@@ -299,11 +299,11 @@ void cp64_plan_gemm(Cp64Plan& pl, const double* A, long long lda, const double* 
   f.X = B; f.ldb = ldb; f.bt = bt; f.tri = tri;
   f.out = C; f.gate = gate;
   const int tm = cdiv64(M, kC64BM), tn = cdiv64(N, kC64BN);
-  // K chunks of >= 64 to bring the units to ~2048 (8 per CU): a 64 x 64 tile's K chain is
+  // K chunks of >= 64 to bring the units to ~1024 (4 per CU): a 64 x 64 tile's K chain is
   // latency-bound at these sizes (each K-step of k_cp64 waits on its staging loads), so short
   // chains side by side beat long ones; the fixed-order reduction reads the extra planes once
   // (with a triangular B most chunks of the early column tiles are empty and return at once)
-  const int by_k = std::max(1, K / 64), by_fill = std::max(1, 2048 / std::max(tm * tn, 1));
+  const int by_k = std::max(1, K / 64), by_fill = std::max(1, 1024 / std::max(tm * tn, 1));
   f.nsplit = std::max(1, std::min(by_k, by_fill));
   f.kchunk = cdiv64(cdiv64(K, f.nsplit), kC64BK) * kC64BK;
   f.nsplit = cdiv64(K, f.kchunk);
@@ -360,7 +360,7 @@ int cp64_launch_job(const Cp64Plan& pl, void* base, int job, hipStream_t s) {
     int pos = 0;
     while (pl.split_ids[pos] != job) ++pos;
     const size_t mn = (size_t)j.M * j.N;
-    const int nb = (int)std::min<size_t>(256, (mn + 255) / 256);
+    const int nb = (int)std::min<size_t>(2048, (mn + 255) / 256);   // (one element per thread up to 512 K)
     hipLaunchKernelGGL(k_cp64_reduce, dim3(nb, 1), dim3(256), 0, s, t.jobs, t.ids + pos);
   }
   return hipGetLastError() == hipSuccess ? ADMMQ_OK : ADMMQ_ERR_HIP;

@@ -55,27 +55,48 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed. One wave: lane r
-// holds row r in registers; the pivot and the column entries l[s][c] are broadcast by
-// readlane, so the 32 right-looking steps need no workgroup barrier.
+__device__ __forceinline__ double shfl_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __shfl((int)b, lane, 64);
+  const int hi = __shfl((int)(b >> 32), lane, 64);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed. One wave, all 64 lanes:
+// lane (r, h) = r + 32 h holds row r's columns 2 j + h in registers, so each of the 32
+// right-looking steps (pivot by readlane, l_r = a_rc / sqrt(pivot), a_rs -= l_r l_s with l_s
+// shuffled from lane s) is about half the instructions per lane of a one-row-per-lane form
+// (which also kept ~60 broadcast values in SGPRs and spilled them): 17.0 -> 10.6 us per
+// block, the same operations per element (same bits; tools/probes/chol_probe.hip). No
+// workgroup barrier inside.
 __device__ void chol32(double* a, int* err) {
-  if (threadIdx.x < NB) {
-    const int r = threadIdx.x;
-    double row[NB];
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x & 31, h = threadIdx.x >> 5;
+    double rw[NB / 2];
 #pragma unroll
-    for (int s = 0; s < NB; ++s) row[s] = a[r * LS + s];
+    for (int j = 0; j < NB / 2; ++j) rw[j] = a[r * LS + 2 * j + h];
 #pragma unroll
     for (int c = 0; c < NB; ++c) {
-      const double d = readlane_d(row[c], c);
-      if (r == 0 && !(d > 0.0)) *err = 1;
+      // row r's entry c lives in lane r + 32 (c & 1), slot c >> 1
+      const double rc = shfl_d(rw[c >> 1], r + 32 * (c & 1));
+      const double d = readlane_d(rw[c >> 1], c + 32 * (c & 1));
+      if (threadIdx.x == 0 && !(d > 0.0)) *err = 1;
       const double sd = sqrt(d);
-      const double l = r > c ? row[c] / sd : (r == c ? sd : 0.0);
-      row[c] = l;
+      const double l = r > c ? rc / sd : (r == c ? sd : 0.0);
+      if ((c & 1) == h) rw[c >> 1] = l;
 #pragma unroll
-      for (int s = c + 1; s < NB; ++s) row[s] -= l * readlane_d(l, s);   // lanes r < s: upper, zeroed below
+      for (int j = 0; j < NB / 2; ++j) {
+        if (2 * j + 1 <= c) continue;   // (uniform: both columns of slot j at or before c)
+        const int sc = 2 * j + h;       // this lane's column of slot j
+        const double ls = shfl_d(l, sc);
+        if (sc > c) rw[j] -= l * ls;
+      }
     }
 #pragma unroll
-    for (int s = 0; s < NB; ++s) a[r * LS + s] = s <= r ? row[s] : 0.0;
+    for (int j = 0; j < NB / 2; ++j) {
+      const int sc = 2 * j + h;
+      a[r * LS + sc] = sc <= r ? rw[j] : 0.0;
+    }
   }
   __syncthreads();
 }

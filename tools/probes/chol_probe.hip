@@ -13,17 +13,13 @@
 #include <cstring>
 #include <vector>
 
-#include "../../admm-quantization_amd/csrc/spd_kernels.hip"
+#include "../../admm-quantization_amd/csrc/spd_kernels.hip"  // (its chol32 is now the w64 form below)
 
 using namespace admmq;
 
-__device__ __forceinline__ double shfl_d(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __shfl((int)b, lane, 64);
-  const int hi = __shfl((int)(b >> 32), lane, 64);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
+// (shfl_d comes with spd_kernels.hip; since round 6 its chol32 is the 64-lane form chol32_w64
+// below, so "chol32" here measures that; the round-6 numbers of the one-row-per-lane form
+// are in profiles/r06_chol_probe.txt)
 __device__ void chol32_shfl(double* a, int* err) {
   if (threadIdx.x < 64) {   // the whole wave takes part in the shuffles; lanes >= 32 idle otherwise
     const int r = threadIdx.x & 31;
@@ -43,6 +39,41 @@ __device__ void chol32_shfl(double* a, int* err) {
     if (threadIdx.x < 32)
 #pragma unroll
       for (int s = 0; s < NB; ++s) a[r * LS + s] = s <= r ? row[s] : 0.0;
+  }
+  __syncthreads();
+}
+
+// chol32 on all 64 lanes: lane (r, h) = r + 32 h holds row r's columns 2 j + h; each step's
+// rank-1 update is ~half as many instructions per lane (the same operations per element:
+// same bits). l_s comes from lane s (which holds l for row s in both halves).
+__device__ void chol32_w64(double* a, int* err) {
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x & 31, h = threadIdx.x >> 5;
+    double rw[NB / 2];
+#pragma unroll
+    for (int j = 0; j < NB / 2; ++j) rw[j] = a[r * LS + 2 * j + h];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      // row r's entry c lives in lane r + 32 (c & 1), slot c >> 1
+      const double rc = shfl_d(rw[c >> 1], r + 32 * (c & 1));
+      const double d = readlane_d(rw[c >> 1], c + 32 * (c & 1));
+      if (threadIdx.x == 0 && !(d > 0.0)) *err = 1;
+      const double sd = sqrt(d);
+      const double l = r > c ? rc / sd : (r == c ? sd : 0.0);
+      if ((c & 1) == h) rw[c >> 1] = l;
+#pragma unroll
+      for (int j = 0; j < NB / 2; ++j) {
+        if (2 * j + 1 <= c) continue;   // (uniform: both columns of slot j at or before c)
+        const int sc = 2 * j + h;       // this lane's column of slot j
+        const double ls = shfl_d(l, sc);
+        if (sc > c) rw[j] -= l * ls;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB / 2; ++j) {
+      const int sc = 2 * j + h;
+      a[r * LS + sc] = sc <= r ? rw[j] : 0.0;
+    }
   }
   __syncthreads();
 }
@@ -93,7 +124,8 @@ __global__ __launch_bounds__(256) void k_p_chol(const ProbDesc* __restrict__ pro
   if (threadIdx.x == 0) err = 0;
   load_block(lkk, p.A64, p.ldm, k, k);
   __syncthreads();
-  if (variant & 1) chol32_shfl(lkk, &err);
+  if (variant & 8) chol32_w64(lkk, &err);
+  else if (variant & 1) chol32_shfl(lkk, &err);
   else chol32(lkk, &err);
   if (variant & 4) {
     if (variant & 2) trinv32_w8(lkk, x);
@@ -120,7 +152,7 @@ int main() {
     ::memset(&h[p], 0, sizeof(ProbDesc));
     CK(hipMalloc(&h[p].A64, a.size() * 8));
     CK(hipMalloc(&h[p].L64, a.size() * 8));
-    CK(hipMalloc(&h[p].D64, (size_t)(nbk + 64 * 9) * 32 * 32 * 8));
+    CK(hipMalloc(&h[p].D64, (size_t)(nbk + 64 * 17) * 32 * 32 * 8));
     CK(hipMalloc(&h[p].flags, 16));
     CK(hipMemset(h[p].flags, 0, 16));
     CK(hipMemcpy(h[p].A64, a.data(), a.size() * 8, hipMemcpyHostToDevice));
@@ -144,9 +176,9 @@ int main() {
     printf("%-40s %9.2f us/launch\n", name, 1000.0 * ms / reps);
   };
   const int reps = 200;
-  const char* names[8] = {"chol32", "chol32_shfl", "", "", "chol32 + trinv32", "chol32_shfl + trinv32", "chol32 + trinv32_w8",
-                          "chol32_shfl + trinv32_w8"};
-  for (int v : {0, 1, 4, 5, 6, 7})
+  const char* names[16] = {"chol32", "chol32_shfl", "", "", "chol32 + trinv32", "chol32_shfl + trinv32", "chol32 + trinv32_w8",
+                           "chol32_shfl + trinv32_w8", "chol32_w64", "", "", "", "chol32_w64 + trinv32", "", "", ""};
+  for (int v : {0, 1, 8, 4, 5, 12, 6, 7})
     timeit(names[v], [&] { hipLaunchKernelGGL(k_p_chol, dim3(nbk, nprob), dim3(256), 0, 0, d, 0, v); }, reps);
   timeit("k_chol_panel (k=0)", [&] { hipLaunchKernelGGL(k_chol_panel, dim3(nbk, nprob), dim3(256), 0, 0, d, 0); }, reps);
   int* bad;
@@ -161,7 +193,9 @@ int main() {
     return 0;
   };
   cmp(0, 1);
+  cmp(0, 8);
   cmp(4, 5);
+  cmp(4, 12);
   cmp(4, 6);
   CK(hipDeviceSynchronize());
   return 0;

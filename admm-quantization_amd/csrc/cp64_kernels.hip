@@ -49,49 +49,91 @@ __device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const bool afast = j.afast != 0, bfast = j.bt != 0;   // bfast: B staged along k (B^T rows contiguous)
-  double ra[kC64PA], rb[kC64PB];
-  auto load = [&](int k0) {
+  // two register sets: the loads of K-step k + 2 are issued before step k's MFMAs, so each has
+  // a whole step of MFMAs plus the barrier to land (one set: the step's own MFMAs only, and
+  // every step then waited on its loads; the same MFMA sequence either way: same bits)
+  double ra[2][kC64PA], rb[2][kC64PB];
+  // the plain GEMM (kind 0, K2 = 1): per-element base pointers formed once, so a K-step's
+  // load is a pointer plus an offset (the generic operand functions divide k by K2 and form
+  // 64-bit products per element and step: VALU work on the MFMA's pipe)
+  const bool plain = j.kind == 0 && j.K2 == 1;
+  const double* pa[kC64PA];
+  const double* pb[kC64PB];
+  int ka[kC64PA], kbq[kC64PB], nb_[kC64PB];
+  long long sa = 0, sb = 0;
+  if (plain) {
+#pragma unroll
+    for (int e = 0; e < kC64PA; ++e) {
+      const int x = tid + kC64NT * e;
+      const int r = afast ? x % kC64BM : x / kC64BK, kk = afast ? x / kC64BM : x % kC64BK;
+      const int m = min(m0 + r, Mrows - 1);
+      pa[e] = j.W + (long long)m * j.sm + (long long)kk * j.s1;
+      ka[e] = m0 + r < Mrows ? kk : (1 << 30);   // past the rows: never loaded
+    }
+    sa = j.s1;
+#pragma unroll
+    for (int e = 0; e < kC64PB; ++e) {
+      const int x = tid + kC64NT * e;
+      const int c = bfast ? x / kC64BK : x % kC64BN, kk = bfast ? x % kC64BK : x / kC64BN;
+      const int n = min(n0 + c, Ncols - 1);
+      pb[e] = j.bt ? j.X + (long long)n * j.ldb + kk : j.X + (long long)kk * j.ldb + n;
+      kbq[e] = n0 + c < Ncols ? kk : (1 << 30);
+      nb_[e] = n0 + c;
+    }
+    sb = j.bt ? 1 : j.ldb;
+  }
+  auto load = [&](int set, int k0) {
+    if (plain) {
+#pragma unroll
+      for (int e = 0; e < kC64PA; ++e) ra[set][e] = k0 + ka[e] < ke ? pa[e][(long long)k0 * sa] : 0.0;
+#pragma unroll
+      for (int e = 0; e < kC64PB; ++e) {
+        const int k = k0 + kbq[e];
+        const bool in = k < ke && (j.tri == 0 || (j.tri == 1 ? k <= nb_[e] : k >= nb_[e]));
+        rb[set][e] = in ? pb[e][(long long)k0 * sb] : 0.0;
+      }
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < kC64PA; ++e) {
       const int x = tid + kC64NT * e;
       const int r = afast ? x % kC64BM : x / kC64BK, kk = afast ? x / kC64BM : x % kC64BK;
       const int m = m0 + r, k = k0 + kk;
-      ra[e] = (m < Mrows && k < ke) ? c64_opA(j, which, m, k) : 0.0;
+      ra[set][e] = (m < Mrows && k < ke) ? c64_opA(j, which, m, k) : 0.0;
     }
 #pragma unroll
     for (int e = 0; e < kC64PB; ++e) {
       const int x = tid + kC64NT * e;
       const int c = bfast ? x / kC64BK : x % kC64BN, kk = bfast ? x % kC64BK : x / kC64BN;
       const int n = n0 + c, k = k0 + kk;
-      rb[e] = (n < Ncols && k < ke) ? c64_opB(j, which, k, n) : 0.0;
+      rb[set][e] = (n < Ncols && k < ke) ? c64_opB(j, which, k, n) : 0.0;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int set, int buf) {
 #pragma unroll
     for (int e = 0; e < kC64PA; ++e) {
       const int x = tid + kC64NT * e;
       const int r = afast ? x % kC64BM : x / kC64BK, kk = afast ? x / kC64BM : x % kC64BK;
-      sA[buf][kk * kC64LD + r] = ra[e];
+      sA[buf][kk * kC64LD + r] = ra[set][e];
     }
 #pragma unroll
     for (int e = 0; e < kC64PB; ++e) {
       const int x = tid + kC64NT * e;
       const int c = bfast ? x / kC64BK : x % kC64BN, kk = bfast ? x % kC64BK : x / kC64BN;
-      sB[buf][kk * kC64LD + c] = rb[e];
+      sB[buf][kk * kC64LD + c] = rb[set][e];
     }
   };
   if (kb >= ke) return;
-  load(kb);
+  load(0, kb);
   __syncthreads();   // the previous use of the images (an earlier core call) is done
-  store(0);
+  store(0, 0);
   __syncthreads();
+  if (kb + kC64BK < ke) load(0, kb + kC64BK);
   int buf = 0;
   const int fr = lane & 15, fk = lane >> 4;   // f64 16x16x4 operands: A[fr][fk], B[fk][fr]
-  for (int k0 = kb; k0 < ke; k0 += kC64BK) {
-    const bool more = k0 + kC64BK < ke;
-    if (more) load(k0 + kC64BK);
-    const double* a = sA[buf] + 32 * wm + fr;
-    const double* b = sB[buf] + 32 * wn + fr;
+  auto mfmas = [&](int bf) {
+    const double* a = sA[bf] + 32 * wm + fr;
+    const double* b = sB[bf] + 32 * wn + fr;
 #pragma unroll
     for (int q = 0; q < kC64BK / 4; ++q) {
       const int kk = (4 * q + fk) * kC64LD;
@@ -101,9 +143,28 @@ __device__ __forceinline__ void c64_core(const Cp64Job& j, int which, int m0, in
       acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
-    if (more) store(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
+  };
+  // step k0 reads LDS image buf; register set s holds step k0 + BK, set s ^ 1 receives k0 + 2 BK
+  for (int k0 = kb; k0 < ke; k0 += 2 * kC64BK) {
+    {
+      const bool more1 = k0 + kC64BK < ke, more2 = k0 + 2 * kC64BK < ke;
+      if (more2) load(1, k0 + 2 * kC64BK);
+      mfmas(buf);
+      if (more1) store(0, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+      if (!more1) break;
+    }
+    {
+      const int k1 = k0 + kC64BK;
+      const bool more1 = k1 + kC64BK < ke, more2 = k1 + 2 * kC64BK < ke;
+      if (more2) load(0, k1 + 2 * kC64BK);
+      mfmas(buf);
+      if (more1) store(1, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+      if (!more1) break;
+    }
   }
 }
 

@@ -292,7 +292,7 @@ def step_roofline(work, max_iter_admm, ms_per_step, num_attempts=200):
             "split_solve_note": "solve term at the split form's f16 MFMA peak / 3 products (838.9 TF/s)"}
 
 
-TRAFFIC_TAGS = ("r05", "r04", "r03")   # newest first
+TRAFFIC_TAGS = ("r06", "r05", "r04", "r03")   # newest first
 
 
 def load_traffic(model, split):

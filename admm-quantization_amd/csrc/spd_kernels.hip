@@ -106,12 +106,17 @@ __device__ void chol32(double* a, int* err) {
 // registers before its FMA chains (read at their use, every LDS read was waited for on
 // its own: 50.6 -> 21.1 us for chol32 + trinv32 over 576 blocks, tools/spd_probe.hip, same
 // bits), and each row's sum runs as two interleaved FMA chains.
+// The 32 reciprocal pivots are divided once, one per thread, into x's spare column 32 (every
+// thread dividing all 32 was ~1000 VALU instructions per thread; the same quotients).
 __device__ __forceinline__ void trinv32(const double* l, double* x) {
   if (threadIdx.x < NB) {
     const int c = threadIdx.x;
+    x[c * LS + NB] = 1.0 / l[c * LS + c];
+    __builtin_amdgcn_wave_barrier();   // (one wave: its LDS writes land before its later reads)
+    asm volatile("" ::: "memory");
     double rinv[NB], col[NB];
 #pragma unroll
-    for (int r = 0; r < NB; ++r) rinv[r] = 1.0 / l[r * LS + r];
+    for (int r = 0; r < NB; ++r) rinv[r] = x[r * LS + NB];
 #pragma unroll
     for (int r = 0; r < NB; ++r) {
       double lr[NB];

@@ -10,7 +10,8 @@
   * all 16 resnet18 3x3 convs: one call of init_factors_many (one stream per layer) against
     the sum of the per-layer calls.
 
-Writes one JSON object to stdout (profiles/r06_epc_init_timing.json)."""
+Writes one JSON object to stdout (profiles/r06_epc_init_timing.json). `--model-only`: only the
+whole-model part (e.g. under GPU_MAX_HW_QUEUES=16, set before the process starts)."""
 import ctypes
 import json
 import os
@@ -24,7 +25,8 @@ from admmq import _lib, panel, synthetic, parafac_epc as pe  # noqa: E402
 
 dev = torch.device("cuda:0")
 lib = _lib.load()
-out = {"steps": [], "layer4": None, "model": None}
+out = {"steps": [], "layer4": None, "model": None, "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
+model_only = "--model-only" in sys.argv
 
 
 def evals(reset=False):
@@ -42,7 +44,7 @@ def sync_time(fn, reps):
     return (time.time() - t0) / reps * 1e3, r
 
 
-for R, m in ((183, 128), (278, 128), (566, 256), (1141, 512), (1141, 9)):
+for R, m in (() if model_only else ((183, 128), (278, 128), (566, 256), (1141, 512), (1141, 9))):
     g = torch.Generator().manual_seed(R)
     B = torch.randn(R, R + 8, generator=g, dtype=torch.float64)
     G = (B @ B.T / (R + 8) + 1e-3 * torch.eye(R, dtype=torch.float64)).to(dev)
@@ -79,18 +81,19 @@ pe.gram_mttkrp_f64 = counted
 idx, spec = synthetic.find_layer("resnet18", "layer4.0.conv2")
 W = torch.from_numpy(synthetic.layer_weight(spec, idx)).to(dev).double()
 R = spec.rank()
-evals(True)
-torch.cuda.synchronize()
-t0 = time.time()
-lam, Us = pe.parafac_epc(W, R, als_maxiter=50, epc_maxiter=50)
-torch.cuda.synchronize()
-t = time.time() - t0
-steps = count["gram_mttkrp"]
-Wc = W.cpu()
-err = float((Wc - pe._reconstruct(lam.cpu(), [u.cpu() for u in Us])).norm() / Wc.norm())
-out["layer4"] = {"layer": "layer4.0.conv2", "R": R, "seconds": round(t, 3), "mode_steps": steps,
-                 "ms_per_mode_step": round(t / max(steps, 1) * 1e3, 3), "epc_evals": evals(True), "rel_err": err}
-print(out["layer4"], file=sys.stderr, flush=True)
+if not model_only:
+    evals(True)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    lam, Us = pe.parafac_epc(W, R, als_maxiter=50, epc_maxiter=50)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    steps = count["gram_mttkrp"]
+    Wc = W.cpu()
+    err = float((Wc - pe._reconstruct(lam.cpu(), [u.cpu() for u in Us])).norm() / Wc.norm())
+    out["layer4"] = {"layer": "layer4.0.conv2", "R": R, "seconds": round(t, 3), "mode_steps": steps,
+                     "ms_per_mode_step": round(t / max(steps, 1) * 1e3, 3), "epc_evals": evals(True), "rel_err": err}
+    print(out["layer4"], file=sys.stderr, flush=True)
 pe.gram_mttkrp_f64 = orig
 
 specs = synthetic.resnet18_layers()
@@ -98,7 +101,7 @@ Ws = [torch.from_numpy(synthetic.layer_weight(s, i)).to(dev).double() for i, s i
 ranks = [s.rank() for s in specs]
 per = []
 torch.cuda.synchronize()
-for Wl, Rl in zip(Ws, ranks):
+for Wl, Rl in zip(Ws, ranks) if not model_only else ():
     t0 = time.time()
     pe.parafac_epc(Wl, Rl, als_maxiter=50, epc_maxiter=50)
     torch.cuda.synchronize()
@@ -109,5 +112,5 @@ res = pe.parafac_epc_many(Ws, ranks, als_maxiter=50, epc_maxiter=50)
 torch.cuda.synchronize()
 t_many = time.time() - t0
 out["model"] = {"model": "resnet18 16 3x3 convs", "per_layer_s": per, "sequential_s": round(sum(per), 3),
-                "concurrent_s": round(t_many, 3), "speedup": round(sum(per) / t_many, 2)}
+                "concurrent_s": round(t_many, 3), "speedup": round(sum(per) / t_many, 2) if per else None}
 print(json.dumps(out))

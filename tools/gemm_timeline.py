@@ -125,3 +125,21 @@ tile_rate = collections.defaultdict(list)
 for r in recs:
     tile_rate[r[8]].append((r[2] - r[1]) / 100)
 print("tile duration by K-steps (mean us, n):", {k: (round(statistics.mean(v), 1), len(v)) for k, v in sorted(tile_rate.items())})
+
+# per-CU tail: the CU's last K-loop end (k_gemm_f32b TRACE builds) against its last tile end,
+# i.e. how long a CU runs after its MFMA work is over (epilogues, stores, atomics)
+if lib.admmq_debug_gemm_trace2(buf2, n) > 0:
+    tails, lastk = [], []
+    for k, v in cus.items():
+        tks = [buf2[2 * x[0]] for x in v if buf2[2 * x[0]] >= x[1]]
+        if not tks:
+            continue
+        tk = max(tks)
+        tails.append((max(x[2] for x in v) - tk) / 100)
+        lastk.append((tk - t0) / 100)
+    tails.sort()
+    lastk.sort()
+    print("CU tail after its last K-loop end (us) percentiles 0/10/50/90/100:",
+          [round(tails[int(q * (len(tails) - 1))], 2) for q in (0, 0.1, 0.5, 0.9, 1.0)])
+    print("CU last K-loop end (us) percentiles 0/10/50/90/100:",
+          [round(lastk[int(q * (len(lastk) - 1))], 1) for q in (0, 0.1, 0.5, 0.9, 1.0)])

@@ -247,6 +247,7 @@ size_t hist3_lds_bytes(int ncand, int bits);
 int copy_hist_trace(unsigned long long* host, int n);
 int copy_gemm_trace(unsigned long long* host, int n);
 int copy_gemm_trace2(unsigned long long* host, int n);
+int copy_gemm_simd(unsigned* host, int n);
 int copy_setup_trace(unsigned long long* host, int n);
 int copy_fin_trace(unsigned long long* host, int n);
 int copy_hist_cu(unsigned long long* host, int n);

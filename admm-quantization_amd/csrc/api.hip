@@ -1648,6 +1648,7 @@ int32_t admmq_admm_run(const admmq_problem* probs, int32_t nprob, int32_t max_it
 int32_t admmq_debug_hist_trace(unsigned long long* host, int32_t n) { return copy_hist_trace(host, n); }
 int32_t admmq_debug_gemm_trace(unsigned long long* host, int32_t n) { return copy_gemm_trace(host, n); }
 int32_t admmq_debug_gemm_trace2(unsigned long long* host, int32_t n) { return copy_gemm_trace2(host, n); }
+int32_t admmq_debug_gemm_simd(unsigned* host, int32_t n) { return copy_gemm_simd(host, n); }
 int32_t admmq_debug_setup_trace(unsigned long long* host, int32_t n) { return copy_setup_trace(host, n); }
 int32_t admmq_debug_fin_trace(unsigned long long* host, int32_t n) { return copy_fin_trace(host, n); }
 int32_t admmq_debug_hist_cu(unsigned long long* host, int32_t n) { return copy_hist_cu(host, n); }

@@ -171,6 +171,12 @@ int copy_gemm_trace2(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace2), (size_t)n * 2 * sizeof(unsigned long long)) == hipSuccess
              ? n : -1;
 }
+// ... and per workgroup the set of SIMDs its waves ran on (bit per SIMD id, k_gemm_f32b)
+__device__ unsigned g_gemm_simd[kGemmTraceMax];
+int copy_gemm_simd(unsigned* host, int n) {
+  n = n < kGemmTraceMax ? n : kGemmTraceMax;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_simd), (size_t)n * sizeof(unsigned)) == hipSuccess ? n : -1;
+}
 int copy_gemm_trace(unsigned long long* host, int n) {
   n = n < kGemmTraceMax ? n : kGemmTraceMax;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess
@@ -736,6 +742,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
   const unsigned long long C0 = ADMMQ_TRACE ? __builtin_amdgcn_s_memtime() : 0ull;
   const GemmTile tl = tiles[blockIdx.x];
   if (tl.nk <= 0) return;   // grid padding (order_tiles_for_cus)
+  if (ADMMQ_TRACE && blockIdx.x < kGemmTraceMax) {   // (uniform over the workgroup)
+    if (tid == 0) g_gemm_simd[blockIdx.x] = 0u;
+    __syncthreads();
+    if (lane == 0) atomicOr(&g_gemm_simd[blockIdx.x], 1u << ((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3));
+  }
   const ProbDesc& p = probs[tl.prob];
   const int ld = tl.ld, ldm = tl.ldm;
   const int row0 = tl.tm * BM, col0 = tl.tn * 64;

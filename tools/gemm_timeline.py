@@ -143,3 +143,16 @@ if lib.admmq_debug_gemm_trace2(buf2, n) > 0:
           [round(tails[int(q * (len(tails) - 1))], 2) for q in (0, 0.1, 0.5, 0.9, 1.0)])
     print("CU last K-loop end (us) percentiles 0/10/50/90/100:",
           [round(lastk[int(q * (len(lastk) - 1))], 1) for q in (0, 0.1, 0.5, 0.9, 1.0)])
+
+# SIMDs each workgroup's four waves ran on (k_gemm_f32b TRACE builds): a CU's 1..3 resident
+# tiles put their waves on distinct SIMDs, or do some share one?
+sfn = getattr(lib, "admmq_debug_gemm_simd", None)
+if sfn is not None:
+    nmax = 8192
+    sb = (ctypes.c_uint * nmax)()
+    if sfn(sb, nmax) > 0:
+        nsimd = collections.Counter(bin(sb[r[0]]).count("1") for r in recs)
+        print("distinct SIMDs per workgroup (4 waves):", dict(sorted(nsimd.items())))
+        lone = [bin(sb[v[0][0]]).count("1") for v in cus.values() if len(v) == 1]
+        if lone:
+            print("  workgroups alone on their CU:", dict(sorted(collections.Counter(lone).items())))

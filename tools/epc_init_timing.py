@@ -11,7 +11,8 @@
     the sum of the per-layer calls.
 
 Writes one JSON object to stdout (profiles/r06_epc_init_timing.json). `--model-only`: only the
-whole-model part (e.g. under GPU_MAX_HW_QUEUES=16, set before the process starts)."""
+whole-model part (e.g. under GPU_MAX_HW_QUEUES=16, set before the process starts);
+`--steps-only`: only the per-step part."""
 import ctypes
 import json
 import os
@@ -27,6 +28,7 @@ dev = torch.device("cuda:0")
 lib = _lib.load()
 out = {"steps": [], "layer4": None, "model": None, "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
 model_only = "--model-only" in sys.argv
+steps_only = "--steps-only" in sys.argv
 
 
 def evals(reset=False):
@@ -77,6 +79,9 @@ def counted(*a, **k):
     return orig(*a, **k)
 
 
+if steps_only:
+    print(json.dumps(out))
+    sys.exit(0)
 pe.gram_mttkrp_f64 = counted
 idx, spec = synthetic.find_layer("resnet18", "layer4.0.conv2")
 W = torch.from_numpy(synthetic.layer_weight(spec, idx)).to(dev).double()

@@ -252,7 +252,10 @@ def epc_step64_gen(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: floa
     device) and yields a ``torch.cuda.Event`` whenever it needs the done flag on the host
     (``EPC_FIRST_ROUNDS`` rounds, then ``EPC_NEXT_ROUNDS`` per read); resume it once the event has
     completed. Returns X = F (G + mu I)^-1; ``mu`` updated in place, ``info`` as ``epc_step64``.
-    ``admmq.parafac_epc`` drives several of these at once, one layer per stream."""
+    The step's search state lives in the current stream's cached workspace, so one stream runs
+    one blocked step (or blocked solve) at a time: finish this generator before the next such
+    call on its stream. ``admmq.parafac_epc`` drives several of these at once, one layer per
+    stream."""
     G, F = _check_solve(G, F, "epc_step64")
     m, n = F.shape
     if mu.dtype != torch.float64 or mu.numel() != 1 or mu.device != F.device:
@@ -267,7 +270,7 @@ def epc_step64_gen(G: torch.Tensor, F: torch.Tensor, normY2: float, delta2: floa
     _lib.check(lib.admmq_epc_begin64(_lib.ptr(G), _lib.ptr(F), m, n, float(normY2), float(delta2), _lib.ptr(mu),
                                      _lib.ptr(X), _lib.ptr(ws), ws.numel(), st), "epc_begin64")
     rounds, total = EPC_FIRST_ROUNDS, 0
-    while total < 96:
+    while total < 96:   # the device search's evaluation budget (kS64MaxEvals, csrc/solve64.hip)
         _lib.check(lib.admmq_epc_rounds64(_lib.ptr(G), _lib.ptr(F), m, n, _lib.ptr(X), rounds, _lib.ptr(done),
                                           _lib.ptr(ws), ws.numel(), st), "epc_rounds64")
         total += rounds

@@ -894,7 +894,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
       const size_t off = (size_t)row * ld + col;
       const float ht = acc[r];
       const float x = ht - upre[r];
+#if ADMMQ_NT_STORES & 4
+      __builtin_nontemporal_store(ht, HTg + off);
+#else
       HTg[off] = ht;
+#endif
       if (Xg) Xg[off] = x;
       if (row < pI && col < pR) {
         amax = max(amax, __float_as_uint(x) & 0x7FFFFFFFu);

@@ -40,7 +40,7 @@ def main():
     solve = sys.argv[4] if len(sys.argv) > 4 else "split"
     fetch, fn = per_dispatch(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write, wn = per_dispatch(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    res = {"source": f"gpurun_out/prof_{tag}_{model} (tools/profile.sh), summarised in profiles/{tag}_{model}_summary.md",
+    res = {"source": f"{os.path.normpath(d)} (tools/profile.sh), summarised in profiles/{tag}_{model}_summary.md",
            "formula": "2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH correction), separate PMC passes",
            "model": model, "split": solve == "split", "classes": {}}
     for cls, pref in CLASSES.items():

@@ -6,12 +6,15 @@
 // -ffp-contract=off so no multiply/add pair is fused behind our back.
 #pragma once
 
-// Outputs written as nontemporal (streamed) stores: bit 0 H / U of the fused finalize, bit 1
-// its next P, bit 2 H_T of the fp32 solve GEMM's epilogue. Default 5: H_T, H and U are read
-// once by the next launches (from the MALL), so leaving them out of the write-back L2 saves
-// the kernel-end write-back of their dirty lines; P stays cached - every column tile of the
-// next solve re-reads it. Same bits either way (C3 per step, three interleaved runs each:
-// 193.7 ms none, 192.9 H_T only, 192.0 H_T + H / U, 192.6 all; profiles/r06_nt_stores_ab.json).
+// Outputs written as nontemporal (streamed) stores: bit 0 H / U of the fused finalize (its
+// two-group form only, NG <= 4: the C3 launches), bit 1 its next P, bit 2 H_T of the fp32
+// solve GEMM's epilogue. Default 5: H_T, H and U are read once by the next launches (from
+// the MALL), so leaving them out of the write-back L2 saves the kernel-end write-back of
+// their dirty lines; P stays cached - every column tile of the next solve re-reads it.
+// Same bits either way. Measured, C3 per step over three interleaved runs each: 193.7 ms
+// none, 192.9 H_T only, 192.0 H_T + H / U, 192.6 all (profiles/r06_nt_stores_ab.json); the
+// three-group form (C4: U re-read with H and F for the finalize) lost 4.7 us per search
+// launch with H / U streamed (42.3 -> 47.0), so it keeps plain stores there.
 #ifndef ADMMQ_NT_STORES
 #define ADMMQ_NT_STORES 5
 #endif
@@ -496,13 +499,13 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
         }
         s1 += (double)a1; s2 += (double)a2; s3 += (double)a3; s4 += (double)a4;
         pv = make_float4(po[0], po[1], po[2], po[3]);
-#if ADMMQ_NT_STORES & 1
-        __builtin_nontemporal_store(hv, (gst4*)(Hd + e));
-        __builtin_nontemporal_store(uv, (gst4*)(Ud + e));
-#else
-        *(gst4*)(Hd + e) = hv;
-        *(gst4*)(Ud + e) = uv;
-#endif
+        if constexpr ((ADMMQ_NT_STORES & 1) != 0 && NG <= 4) {   // (see ADMMQ_NT_STORES)
+          __builtin_nontemporal_store(hv, (gst4*)(Hd + e));
+          __builtin_nontemporal_store(uv, (gst4*)(Ud + e));
+        } else {
+          *(gst4*)(Hd + e) = hv;
+          *(gst4*)(Ud + e) = uv;
+        }
 #if ADMMQ_NT_STORES & 2
         if (!split) __builtin_nontemporal_store(gf32x4{pv.x, pv.y, pv.z, pv.w}, (gst4*)(Pd + e));
         else

@@ -3,7 +3,7 @@
 # lines, the emulated 8-rank shards of resnet18 / resnet50, and the EPC initialiser timing.
 # Each step under its own time limit; the session stops at the first failure.
 cd "$(dirname "$0")/.." || exit 1
-T=gpurun_out/r06q
+T=gpurun_out/${1:-r06q}
 mkdir -p gpurun_out
 set -o pipefail
 timeout -k 10 300 python3 -u bench.py > ${T}_bench_default.json 2> ${T}_bench_default.err || exit 3

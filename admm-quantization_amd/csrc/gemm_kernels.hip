@@ -883,7 +883,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
   if constexpr (!PRE) load_u();
   unsigned amax = 0u, mn = 0xFFFFFFFFu, mxo = 0u;
   typedef __attribute__((address_space(1))) float gf32;
-  gf32* const HTg = (gf32*)p.HT;
+  [[maybe_unused]] gf32* const HTg = (gf32*)p.HT;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t htrs = __builtin_amdgcn_make_buffer_rsrc(p.HT, 0, 0x7FFFFFFF, 0x00020000);
   gf32* const Xg = p.X_dbg ? (gf32*)p.X : nullptr;   // debug output only
   const int pI = p.I, pR = p.R;
   const int col = col0 + 32 * wn + i;
@@ -894,7 +895,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 4
       const size_t off = (size_t)row * ld + col;
       const float ht = acc[r];
       const float x = ht - upre[r];
-#if ADMMQ_NT_STORES & 4
+#if ADMMQ_SC1_STORES & 4
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ht), htrs, (int)(off * 4), 0, 16);
+#elif ADMMQ_NT_STORES & 4
       __builtin_nontemporal_store(ht, HTg + off);
 #else
       HTg[off] = ht;

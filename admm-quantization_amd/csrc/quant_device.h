@@ -6,17 +6,22 @@
 // -ffp-contract=off so no multiply/add pair is fused behind our back.
 #pragma once
 
-// Outputs written as nontemporal (streamed) stores: bit 0 H / U of the fused finalize (its
-// two-group form only, NG <= 4: the C3 launches), bit 1 its next P, bit 2 H_T of the fp32
-// solve GEMM's epilogue. Default 5: H_T, H and U are read once by the next launches (from
-// the MALL), so leaving them out of the write-back L2 saves the kernel-end write-back of
-// their dirty lines; P stays cached - every column tile of the next solve re-reads it.
-// Same bits either way. Measured, C3 per step over three interleaved runs each: 193.7 ms
-// none, 192.9 H_T only, 192.0 H_T + H / U, 192.6 all (profiles/r06_nt_stores_ab.json); the
-// three-group form (C4: U re-read with H and F for the finalize) lost 4.7 us per search
-// launch with H / U streamed (42.3 -> 47.0), so it keeps plain stores there.
+// Store policy of the per-iteration outputs (same bits under every policy; C3 / C4 per step,
+// interleaved runs, profiles/r06_nt_stores_ab.json and r06_store_policy_ab.json):
+// ADMMQ_SC1_STORES (default 7): write-through (sc1) stores - bit 0 H / U of the fused
+// finalize, bit 1 its next P, bit 2 H_T of the fp32 solve GEMM's epilogue. Every one of them
+// is read by the next launch; written through, its lines reach the MALL as they are stored,
+// so a kernel's end has no dirty L2 lines to write back (on MI355X the eight XCD L2s are
+// written back at every kernel's release), while they stay valid in the writing XCD's L2.
+// C3 192.6 -> 187.8 ms (GEMM 49.0 -> 47.9 us, search 30.5 -> 29.0), C4 241.0 -> 239.9 ms.
+// ADMMQ_NT_STORES (bits as above; used where SC1 is off): nontemporal stores, which skip L2
+// instead - 193.7 -> 192.0 ms at C3 for H_T + H / U, but the C4 search lost 4.7 us with H / U
+// streamed (its finalize re-reads U, H, F), so H / U stream only in the two-group form.
 #ifndef ADMMQ_NT_STORES
 #define ADMMQ_NT_STORES 5
+#endif
+#ifndef ADMMQ_SC1_STORES
+#define ADMMQ_SC1_STORES 7
 #endif
 #include "admmq_internal.h"
 
@@ -469,6 +474,10 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
   const int lane = threadIdx.x & 63;
   if constexpr (STREAM) {
+    typedef unsigned sc1u4 __attribute__((ext_vector_type(4)));
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(Hd, 0, 0x7FFFFFFF, 0x00020000);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(Ud, 0, 0x7FFFFFFF, 0x00020000);
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(Pd, 0, 0x7FFFFFFF, 0x00020000);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the inputs are complete: stores below wait for nothing
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -499,14 +508,20 @@ __device__ __forceinline__ void admm_finalize_block(const ProbDesc& p, long long
         }
         s1 += (double)a1; s2 += (double)a2; s3 += (double)a3; s4 += (double)a4;
         pv = make_float4(po[0], po[1], po[2], po[3]);
-        if constexpr ((ADMMQ_NT_STORES & 1) != 0 && NG <= 4) {   // (see ADMMQ_NT_STORES)
+        if constexpr ((ADMMQ_SC1_STORES & 1) != 0) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc1u4, hv), hrs, e * 4, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc1u4, uv), urs, e * 4, 0, 16);
+        } else if constexpr ((ADMMQ_NT_STORES & 1) != 0 && NG <= 4) {   // (see ADMMQ_NT_STORES)
           __builtin_nontemporal_store(hv, (gst4*)(Hd + e));
           __builtin_nontemporal_store(uv, (gst4*)(Ud + e));
         } else {
           *(gst4*)(Hd + e) = hv;
           *(gst4*)(Ud + e) = uv;
         }
-#if ADMMQ_NT_STORES & 2
+#if ADMMQ_SC1_STORES & 2
+        if (!split) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc1u4, gf32x4{pv.x, pv.y, pv.z, pv.w}), prs, e * 4, 0, 16);
+        else
+#elif ADMMQ_NT_STORES & 2
         if (!split) __builtin_nontemporal_store(gf32x4{pv.x, pv.y, pv.z, pv.w}, (gst4*)(Pd + e));
         else
 #endif

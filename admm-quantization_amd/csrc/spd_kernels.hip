@@ -64,15 +64,12 @@ __device__ __forceinline__ double shfl_d(double v, int lane) {
 
 // In-LDS Cholesky of a 32x32 SPD block (lower); upper part zeroed. One wave, all 64 lanes:
 // lane (r, h) = r + 32 h holds row r's columns 2 j + h in registers, so each of the 32
-// right-looking steps (pivot by readlane, l_r = a_rc / sqrt(pivot), a_rs -= l_r l_s) is about
-// half the instructions per lane of a one-row-per-lane form (17.0 -> 10.6 us per block).
-// The column's l values reach the lanes through LDS: lane (r, 0) stores l_r into the parity
-// array of r and every lane reads the 16 l_s of its own parity (one store and one read round
-// per column instead of 16 shuffles per lane: 14.7 -> 10.4 us per block in the same probe
-// run). The same operations per element either way (same bits; tools/probes/chol_probe.hip).
-// No workgroup barrier inside.
+// right-looking steps (pivot by readlane, l_r = a_rc / sqrt(pivot), a_rs -= l_r l_s with l_s
+// shuffled from lane s) is about half the instructions per lane of a one-row-per-lane form
+// (which also kept ~60 broadcast values in SGPRs and spilled them): 17.0 -> 10.6 us per
+// block, the same operations per element (same bits; tools/probes/chol_probe.hip). No
+// workgroup barrier inside.
 __device__ void chol32(double* a, int* err) {
-  __shared__ double lb[2][NB / 2];
   if (threadIdx.x < 64) {
     const int r = threadIdx.x & 31, h = threadIdx.x >> 5;
     double rw[NB / 2];
@@ -87,19 +84,13 @@ __device__ void chol32(double* a, int* err) {
       const double sd = sqrt(d);
       const double l = r > c ? rc / sd : (r == c ? sd : 0.0);
       if ((c & 1) == h) rw[c >> 1] = l;
-      if (h == 0) lb[r & 1][r >> 1] = l;
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS stores landed
-      __builtin_amdgcn_wave_barrier();
-      double ls[NB / 2];
-#pragma unroll
-      for (int j = 0; j < NB / 2; ++j) ls[j] = lb[h][j];   // l_{2j+h}
 #pragma unroll
       for (int j = 0; j < NB / 2; ++j) {
         if (2 * j + 1 <= c) continue;   // (uniform: both columns of slot j at or before c)
         const int sc = 2 * j + h;       // this lane's column of slot j
-        if (sc > c) rw[j] -= l * ls[j];
+        const double ls = shfl_d(l, sc);
+        if (sc > c) rw[j] -= l * ls;
       }
-      __builtin_amdgcn_wave_barrier();      // every lane has read lb before the next column's stores
     }
 #pragma unroll
     for (int j = 0; j < NB / 2; ++j) {

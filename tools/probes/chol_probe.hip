@@ -17,9 +17,9 @@
 
 using namespace admmq;
 
-// (shfl_d comes with spd_kernels.hip; its chol32 is the 64-lane form with the LDS broadcast;
-// chol32_w64 below is the same form with shuffles, its predecessor; the round-6 numbers of
-// the one-row-per-lane form are in profiles/r06_chol_probe.txt)
+// (shfl_d comes with spd_kernels.hip; since round 6 its chol32 is the 64-lane form chol32_w64
+// below, so "chol32" here measures that; the round-6 numbers of the one-row-per-lane form
+// are in profiles/r06_chol_probe.txt)
 __device__ void chol32_shfl(double* a, int* err) {
   if (threadIdx.x < 64) {   // the whole wave takes part in the shuffles; lanes >= 32 idle otherwise
     const int r = threadIdx.x & 31;
@@ -124,19 +124,14 @@ __global__ __launch_bounds__(256) void k_p_chol(const ProbDesc* __restrict__ pro
   if (threadIdx.x == 0) err = 0;
   load_block(lkk, p.A64, p.ldm, k, k);
   __syncthreads();
-  if (variant == 2 || variant == 3) {   // 2: chol32 (the library's LDS-broadcast form), 3: + trinv32
-    chol32(lkk, &err);
-    if (variant == 3) trinv32(lkk, x);
-  } else {
-    if (variant & 8) chol32_w64(lkk, &err);
-    else if (variant & 1) chol32_shfl(lkk, &err);
-    else chol32(lkk, &err);
-    if (variant & 4) {
-      if (variant & 2) trinv32_w8(lkk, x);
-      else trinv32(lkk, x);
-    }
+  if (variant & 8) chol32_w64(lkk, &err);
+  else if (variant & 1) chol32_shfl(lkk, &err);
+  else chol32(lkk, &err);
+  if (variant & 4) {
+    if (variant & 2) trinv32_w8(lkk, x);
+    else trinv32(lkk, x);
   }
-  if (i == k) store_block(p.D64 + (size_t)32 * 32 * 64 * (variant + 1), NB, k, 0, ((variant & 4) || variant == 3) ? x : lkk);
+  if (i == k) store_block(p.D64 + (size_t)32 * 32 * 64 * (variant + 1), NB, k, 0, (variant & 4) ? x : lkk);
 }
 
 __global__ void k_cmp(const double* a, const double* b, int n, int* bad, double* maxrel) {
@@ -181,9 +176,9 @@ int main() {
     printf("%-40s %9.2f us/launch\n", name, 1000.0 * ms / reps);
   };
   const int reps = 200;
-  const char* names[16] = {"chol32", "chol32_shfl", "chol32 (library)", "chol32 (library) + trinv32", "chol32 + trinv32", "chol32_shfl + trinv32", "chol32 + trinv32_w8",
+  const char* names[16] = {"chol32", "chol32_shfl", "", "", "chol32 + trinv32", "chol32_shfl + trinv32", "chol32 + trinv32_w8",
                            "chol32_shfl + trinv32_w8", "chol32_w64", "", "", "", "chol32_w64 + trinv32", "", "", ""};
-  for (int v : {8, 2, 12, 3})
+  for (int v : {0, 1, 8, 4, 5, 12, 6, 7})
     timeit(names[v], [&] { hipLaunchKernelGGL(k_p_chol, dim3(nbk, nprob), dim3(256), 0, 0, d, 0, v); }, reps);
   timeit("k_chol_panel (k=0)", [&] { hipLaunchKernelGGL(k_chol_panel, dim3(nbk, nprob), dim3(256), 0, 0, d, 0); }, reps);
   int* bad;
@@ -197,8 +192,11 @@ int main() {
     printf("%s vs %s: %d differing doubles\n", names[va], names[vb], hb);
     return 0;
   };
-  cmp(8, 2);
-  cmp(12, 3);
+  cmp(0, 1);
+  cmp(0, 8);
+  cmp(4, 5);
+  cmp(4, 12);
+  cmp(4, 6);
   CK(hipDeviceSynchronize());
   return 0;
 }
